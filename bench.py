@@ -1,0 +1,189 @@
+"""Benchmark: grasp-pose IK solves/sec (Nextage dual-arm) on 1..8 MI355X.
+
+    python bench.py [--gpus N --steps K --warmup W --batch B --dtype f64|f32]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A step = one launch of the batched IK kernel over this rank's batch of
+synthetic grasp targets (already resident in HBM) plus, for N > 1, the RCCL
+gather of the final q to rank 0 (north star: "at most an RCCL gather of the
+final q over xGMI").  Weak scaling: every rank solves `--batch` targets.
+Default workload = BASELINE.json configs[1]: 4,096 targets, fp64, 1 GPU.
+
+`value` counts CONVERGED solves per second over all ranks (the metric's
+unit); all problems/s is reported beside it.  The dominant kernel's roofline
+is VALU (fp64/fp32 vector ALU, no MFMA, negligible HBM traffic) — see
+DESIGN.md §5; the HBM figure the north star asks for is reported as
+`roofline_hbm`.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd"))
+
+METRIC = "grasp-pose IK solves/sec (Nextage dual-arm) at 1/2/4/8 MI355X"
+F_ITER = 3144  # FP ops per IK iteration
+PEAK_VALU = {"f64": 78.6, "f32": 157.3}  # TFLOP/s vector peaks (MI355X spec)
+PEAK_HBM = 8000.0  # GB/s (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes(dtype, B, nq=15, broadcast_q0=True):
+    """HBM bytes one launch must move: targets + q0 + q + iters + flag + err."""
+    s = 8 if dtype == "f64" else 4
+    q0 = nq * s if broadcast_q0 else nq * s * B
+    return B * (12 * s + nq * s + 4 + 1 + 2 * s) + q0
+
+
+def cpu_baseline(targets, budget_s=12.0):
+    """Time the C restatement (oracle/ikg_oracle.c) on host cores over a
+    bounded prefix of the same workload."""
+    sys.path.insert(0, ROOT)
+    from oracle import c_oracle
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = min(threads, 16)
+    n_cal = min(len(targets), 8 * threads)
+    t0 = time.perf_counter()
+    c_oracle.solve(targets[:n_cal], np.zeros(15), threads=threads)
+    per = (time.perf_counter() - t0) / n_cal
+    n = int(min(len(targets), max(n_cal, budget_s / max(per, 1e-9))))
+    t0 = time.perf_counter()
+    _, conv, iters, _ = c_oracle.solve(targets[:n], np.zeros(15), threads=threads)
+    dt = time.perf_counter() - t0
+    return {
+        "value": float(conv.sum() / dt), "unit": "converged solves/s", "cores": threads, "kind": "port",
+        "sample": f"first {n} of the {len(targets)} benchmark targets, q0=0, fp64 C restatement "
+                  f"(oracle/ikg_oracle.c, OpenMP), {dt:.1f} s; all-problem rate {n / dt:.1f}/s",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=4096, help="targets per GPU (weak scaling)")
+    ap.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    ap.add_argument("--yaw", type=float, default=0.0, help="random yaw range (rad) of the cube targets")
+    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--variant", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from ikgrasp import _lib
+    from ikgrasp.solver import IKSolver
+    from ikgrasp.workload import uniform_targets
+
+    solver = IKSolver(device=local)
+    B = args.batch
+    tg_np = uniform_targets(B, seed=rank, yaw=args.yaw)
+    tdt = torch.float64 if args.dtype == "f64" else torch.float32
+    code = _lib.IKG_F64 if args.dtype == "f64" else _lib.IKG_F32
+    targets = torch.tensor(tg_np, dtype=tdt, device=dev)
+    q0 = torch.zeros(15, dtype=tdt, device=dev)
+    q_out = torch.empty((B, 15), dtype=tdt, device=dev)
+    conv = torch.empty(B, dtype=torch.uint8, device=dev)
+    iters = torch.empty(B, dtype=torch.int32, device=dev)
+    err = torch.empty((B, 2), dtype=tdt, device=dev)
+    gathered = [torch.empty_like(q_out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        solver.solve_into(targets, q0, q_out, conv, iters, err, code, sh, variant=args.variant)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1 and not args.no_gather:
+            dist.gather(q_out, gathered, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+
+    n_conv = int(conv.sum().item())
+    sum_iters = int(iters.to(torch.int64).sum().item())
+    stats = torch.tensor([elapsed, kern_ms, n_conv, B, sum_iters], dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = stats[:2].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        counts = stats[2:].clone()
+        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
+        stats = torch.cat([t_max, counts])
+    elapsed, kern_ms, tot_conv, tot_B, tot_iters = stats.tolist()
+
+    if rank == 0:
+        per_step = elapsed / args.steps
+        value = tot_conv / per_step
+        flops = (sum_iters * F_ITER) / (kern_ms * 1e-3) / 1e12  # rank-0 kernel, TFLOP/s
+        abytes = algorithmic_bytes(args.dtype, B)
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.dtype}_b{B}.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        out = {
+            "metric": METRIC, "value": value, "unit": "converged solves/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_step * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (cube targets ~ path.py:35-47 sampler, seed = rank; q0 = robot.q0 = 0)",
+            "config": {
+                "workload": (f"BASELINE configs[1]: batch {B} grasp targets per GPU, {args.dtype}, "
+                             f"pair kernel (2 lanes/problem)"),
+                "batch_per_gpu": B, "global_batch": B * world, "yaw_range": args.yaw,
+                "parallelism": f"shard{world}" + ("" if world == 1 or args.no_gather else "+rccl_gather_q"),
+            },
+            "problems_per_s": tot_B / per_step,
+            "converged_fraction": tot_conv / tot_B,
+            "mean_iters": tot_iters / tot_B,
+            "roofline": {
+                "bound": "valu", "achieved": flops, "peak": PEAK_VALU[args.dtype], "unit": "TFLOP/s",
+                "frac": flops / PEAK_VALU[args.dtype], "traffic": traffic,
+                "kernel": "ikg_pair_batch_kernel", "kernel_ms": kern_ms,
+                "work": f"sum(iters)={sum_iters} x {F_ITER} FP ops (SURVEY §8a)",
+            },
+            "roofline_hbm": {
+                "bound": "hbm", "achieved": abytes / (kern_ms * 1e-3) / 1e9, "peak": PEAK_HBM, "unit": "GB/s",
+                "frac": abytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM, "traffic": traffic,
+                "algorithmic_bytes": abytes,
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(tg_np)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    solver.close()
+
+
+if __name__ == "__main__":
+    main()

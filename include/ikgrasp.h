@@ -1,0 +1,144 @@
+/*
+ * ikgrasp — MI355X-native batched dual-arm grasp-pose inverse kinematics.
+ *
+ * C-ABI of libikgrasp.so (plain pointers and sizes; no C++ or torch types).
+ * It replaces the per-call Pinocchio loop of the reference:
+ *
+ *   computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None)
+ *       /root/reference/inverse_geometry.py:17-100
+ *
+ * whose Python->C++ crossings (pin.framesForwardKinematics :58,
+ * pin.computeJointJacobians :59, pin.log :66-67, pin.computeFrameJacobian
+ * :75-76, np.linalg.pinv :83, pin.integrate :86, projecttojointlimits :89 ->
+ * tools.py:21-22) are fused into one HIP kernel launch over a batch.
+ * The ctypes binding a maintainer adds on the reference side is shown in
+ * INTEGRATION.md.
+ *
+ * Conventions
+ *   - SE(3) placements are 12 scalars: R row-major (9) then t (3).
+ *   - Motion vectors are [linear; angular] (Pinocchio convention).
+ *   - Float arrays use the dtype selected by `dtype` (IKG_F64 / IKG_F32).
+ *   - All buffers are owned by the caller.  They are device pointers unless
+ *     IKG_FLAG_HOST_POINTERS is set, in which case the library stages them
+ *     through device scratch and synchronises the stream before returning.
+ *   - Return 0 on success, a negative IKG_E* code on failure; the message of
+ *     the last failure on the calling thread is ikg_last_error().  Nothing
+ *     throws or exits across this boundary.
+ *   - Calls are re-entrant per (model, stream).
+ */
+#ifndef IKGRASP_H
+#define IKGRASP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IKG_MAX_NQ 32
+#define IKG_ARM_DOF 6
+
+enum ikg_dtype { IKG_F64 = 0, IKG_F32 = 1 };
+
+enum ikg_status {
+  IKG_OK = 0,
+  IKG_EINVAL = -1,      /* bad argument / unsupported model structure */
+  IKG_EHIP = -2,        /* HIP runtime error */
+  IKG_ENOMEM = -3,      /* device allocation failed */
+  IKG_ENODEV = -4       /* no such device */
+};
+
+/* flags */
+#define IKG_FLAG_HOST_POINTERS 1u
+
+/* kernel variant selector (ikg_params.variant) */
+enum ikg_variant {
+  IKG_VARIANT_AUTO = 0,  /* choose by batch size / occupancy */
+  IKG_VARIANT_PAIR = 1,  /* two lanes per problem (one arm per lane), 32 problems / wave */
+  IKG_VARIANT_WAVE = 2   /* cooperative: 16 lanes per problem, 4 problems / wave */
+};
+
+/* Robot + grasp-object description (produced by the model compiler,
+ * ikgrasp/model.py, from the URDFs — setup_pinocchio.py:73-83). */
+typedef struct ikg_model_desc {
+  int32_t nq;                        /* configuration size (15 for Nextage) */
+  int32_t parent[IKG_MAX_NQ];        /* parent joint (q index), -1 = universe */
+  int32_t axis[IKG_MAX_NQ];          /* 0/1/2 = revolute about +X/+Y/+Z */
+  double placement[IKG_MAX_NQ][12];  /* joint placement in parent frame (R row-major, t) */
+  double lower[IKG_MAX_NQ];          /* joint limits (projecttojointlimits, tools.py:21-22) */
+  double upper[IKG_MAX_NQ];
+  int32_t root_q;                    /* shared joint feeding both arms (chest) */
+  int32_t arm_q[2][IKG_ARM_DOF];     /* left/right arm joints, proximal -> distal */
+  double hand[2][12];                /* LARM_EFF / RARM_EFF frame in last arm joint frame */
+  double hook[2][12];                /* LARM_HOOK / RARM_HOOK in the cube frame (cube_small.urdf:34-47) */
+} ikg_model_desc;
+
+/* Loop hyper-parameters; defaults equal the reference
+ * (EPSILON config.py:22, DT and max_iters inverse_geometry.py:53-54). */
+typedef struct ikg_params {
+  double eps;          /* stop when |log6 err| < eps for both hands (1e-3) */
+  double dt;           /* q <- clip(q + dt * dq) (1e-2) */
+  int32_t max_iters;   /* joint updates before giving up (1000) */
+  int32_t variant;     /* enum ikg_variant */
+  double lambda;       /* damping of (J J^T + lambda I); 0 = pinv semantics (reference) */
+} ikg_params;
+
+typedef struct ikg_model ikg_model;
+
+/* Build a device-ready model (tables are uploaded to every device lazily). */
+int ikg_model_create(const ikg_model_desc* desc, ikg_model** out);
+void ikg_model_destroy(ikg_model* model);
+
+/* Fill `p` with the reference defaults. */
+void ikg_params_default(ikg_params* p);
+
+/*
+ * Batched computeqgrasppose (inverse_geometry.py:17-100, collision term
+ * excluded — see DESIGN.md §8f-1).
+ *   targets   [B,12]  cube placements (cubetarget); hooks are applied inside
+ *   q0        [B,nq] (q0_stride = nq) or [nq] broadcast (q0_stride = 0)
+ *   q_out     [B,nq]  first iterate with both errors < eps, else the iterate
+ *                     after max_iters updates (same as the reference)
+ *   converged [B]     1 if the stop test passed (reference `success` without
+ *                     the collision term)
+ *   iters     [B]     joint updates performed (may be NULL)
+ *   err_out   [B,2]   |log6| of left/right hand at q_out (may be NULL)
+ */
+int ikg_solve_batch(const ikg_model* model, int device, int dtype,
+                    const void* targets, const void* q0, int64_t q0_stride, int64_t B,
+                    const ikg_params* params,
+                    void* q_out, uint8_t* converged, int32_t* iters, void* err_out,
+                    void* stream, uint32_t flags);
+
+/*
+ * Multi-start: every target is solved from every seed (S seeds x T targets);
+ * per target the best seed is kept: lowest max(|eL|,|eR|) among converged
+ * seeds, else lowest overall (ties -> lowest seed index).
+ *   seeds [S,nq]; outputs per target: q_out [T,nq], converged [T], iters [T],
+ *   err_out [T,2], best_seed [T] (any output but q_out may be NULL).
+ */
+int ikg_solve_multistart(const ikg_model* model, int device, int dtype,
+                         const void* targets, int64_t T, const void* seeds, int64_t S,
+                         const ikg_params* params,
+                         void* q_out, uint8_t* converged, int32_t* iters, void* err_out,
+                         int32_t* best_seed, void* stream, uint32_t flags);
+
+/*
+ * Batched effector forward kinematics (pin.framesForwardKinematics +
+ * data.oMf[LARM_EFF/RARM_EFF], inverse_geometry.py:58-63).
+ *   q [B,nq] -> hands [B,2,12]
+ */
+int ikg_fk_batch(const ikg_model* model, int device, int dtype,
+                 const void* q, int64_t B, void* hands, void* stream, uint32_t flags);
+
+/* Thread-local message of the last failure ("" if none). */
+const char* ikg_last_error(void);
+
+/* Library version string. */
+const char* ikg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* IKGRASP_H */

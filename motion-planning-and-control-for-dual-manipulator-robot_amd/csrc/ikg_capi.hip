@@ -1,0 +1,438 @@
+// C-ABI of libikgrasp.so (include/ikgrasp.h).
+//
+// Owns model validation / upload, argument checking, optional host staging
+// and kernel dispatch.  No exception or exit crosses the boundary: every
+// failure returns a negative code and leaves a message in ikg_last_error().
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "ikg_device.hpp"
+#include "ikg_launch.hpp"
+#include "ikgrasp.h"
+
+namespace {
+
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(IKG_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+bool is_identity(const double* R) {
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      if (R[3 * r + c] != (r == c ? 1.0 : 0.0)) return false;
+  return true;
+}
+
+template <typename T>
+void build_kmodel(const ikg_model_desc& d, ikg::KModel<T>& k) {
+  std::memset(&k, 0, sizeof(k));
+  const int r = d.root_q;
+  for (int i = 0; i < 9; ++i) k.root_R[i] = (T)d.placement[r][i];
+  for (int i = 0; i < 3; ++i) k.root_t[i] = (T)d.placement[r][9 + i];
+  k.root_lo = (T)d.lower[r];
+  k.root_hi = (T)d.upper[r];
+  k.root_q = r;
+  k.root_axis = d.axis[r];
+  k.rot_mask = 0;
+  for (int a = 0; a < 2; ++a)
+    for (int j = 0; j < IKG_ARM_DOF; ++j) {
+      const int q = d.arm_q[a][j];
+      for (int i = 0; i < 9; ++i) k.arm_R[a][j][i] = (T)d.placement[q][i];
+      for (int i = 0; i < 3; ++i) k.arm_t[a][j][i] = (T)d.placement[q][9 + i];
+      k.arm_lo[a][j] = (T)d.lower[q];
+      k.arm_hi[a][j] = (T)d.upper[q];
+      k.arm_q[a][j] = q;
+      k.arm_axis[j] = d.axis[q];
+      if (!is_identity(d.placement[q])) k.rot_mask |= 1 << j;
+    }
+  for (int a = 0; a < 2; ++a) {
+    for (int i = 0; i < 9; ++i) k.hand_R[a][i] = (T)d.hand[a][i];
+    for (int i = 0; i < 3; ++i) k.hand_t[a][i] = (T)d.hand[a][9 + i];
+    for (int i = 0; i < 9; ++i) k.hook_R[a][i] = (T)d.hook[a][i];
+    for (int i = 0; i < 3; ++i) k.hook_t[a][i] = (T)d.hook[a][9 + i];
+  }
+  for (int q = 0; q < d.nq; ++q) {
+    k.lo[q] = (T)d.lower[q];
+    k.hi[q] = (T)d.upper[q];
+  }
+  k.nq = d.nq;
+  bool used[IKG_MAX_NQ] = {};
+  used[r] = true;
+  for (int a = 0; a < 2; ++a)
+    for (int j = 0; j < IKG_ARM_DOF; ++j) used[d.arm_q[a][j]] = true;
+  k.n_passive = 0;
+  for (int q = 0; q < d.nq; ++q)
+    if (!used[q]) k.passive_q[k.n_passive++] = q;
+}
+
+}  // namespace
+
+struct ikg_model {
+  ikg_model_desc desc;
+  ikg::KModel<double> k64;
+  ikg::KModel<float> k32;
+  std::mutex mu;
+  std::vector<void*> dev64;  // per device
+  std::vector<void*> dev32;
+
+  template <typename T>
+  int device_tables(int device, const ikg::KModel<T>** out) {
+    std::lock_guard<std::mutex> lock(mu);
+    std::vector<void*>& slot = sizeof(T) == 8 ? dev64 : dev32;
+    if ((int)slot.size() <= device) slot.resize(device + 1, nullptr);
+    if (!slot[device]) {
+      void* p = nullptr;
+      hipError_t e = hipMalloc(&p, sizeof(ikg::KModel<T>));
+      if (e != hipSuccess) return fail(IKG_ENOMEM, "hipMalloc(model tables): %s", hipGetErrorString(e));
+      const void* src = sizeof(T) == 8 ? (const void*)&k64 : (const void*)&k32;
+      e = hipMemcpy(p, src, sizeof(ikg::KModel<T>), hipMemcpyHostToDevice);
+      if (e != hipSuccess) {
+        (void)hipFree(p);
+        return hip_fail(e, "hipMemcpy(model tables)");
+      }
+      slot[device] = p;
+    }
+    *out = (const ikg::KModel<T>*)slot[device];
+    return IKG_OK;
+  }
+};
+
+namespace {
+
+// Select and restore the current device around a call.
+struct DeviceGuard {
+  int prev = -1;
+  int rc = IKG_OK;
+  explicit DeviceGuard(int device) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+      rc = hip_fail(e, "hipGetDeviceCount");
+      return;
+    }
+    if (device < 0 || device >= n) {
+      rc = fail(IKG_ENODEV, "device %d out of range (%d visible)", device, n);
+      return;
+    }
+    (void)hipGetDevice(&prev);
+    e = hipSetDevice(device);
+    if (e != hipSuccess) rc = hip_fail(e, "hipSetDevice");
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// Stages host buffers through device scratch when IKG_FLAG_HOST_POINTERS is set.
+struct Staging {
+  std::vector<void*> allocs;
+  hipStream_t s;
+  int rc = IKG_OK;
+  explicit Staging(hipStream_t st) : s(st) {}
+  ~Staging() {
+    for (void* p : allocs) (void)hipFree(p);
+  }
+  void* in(const void* host, size_t bytes) {
+    if (!host || rc) return nullptr;
+    void* d = nullptr;
+    hipError_t e = hipMalloc(&d, bytes ? bytes : 1);
+    if (e != hipSuccess) {
+      rc = fail(IKG_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+      return nullptr;
+    }
+    allocs.push_back(d);
+    if (bytes) {
+      e = hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync(H2D)");
+    }
+    return d;
+  }
+  void* out(size_t bytes) { return in_alloc(bytes); }
+  void* in_alloc(size_t bytes) {
+    if (rc) return nullptr;
+    void* d = nullptr;
+    hipError_t e = hipMalloc(&d, bytes ? bytes : 1);
+    if (e != hipSuccess) {
+      rc = fail(IKG_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+      return nullptr;
+    }
+    allocs.push_back(d);
+    return d;
+  }
+  int back(void* host, const void* dev, size_t bytes) {
+    if (!host || !dev || rc) return rc;
+    hipError_t e = hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync(D2H)");
+    return rc;
+  }
+};
+
+int check_params(const ikg_params* p) {
+  if (!p) return fail(IKG_EINVAL, "params is NULL");
+  if (!(p->eps > 0) || !std::isfinite(p->eps)) return fail(IKG_EINVAL, "eps must be > 0");
+  if (!std::isfinite(p->dt)) return fail(IKG_EINVAL, "dt must be finite");
+  if (p->max_iters < 0) return fail(IKG_EINVAL, "max_iters must be >= 0");
+  if (!(p->lambda >= 0) || !std::isfinite(p->lambda)) return fail(IKG_EINVAL, "lambda must be >= 0");
+  if (p->variant != IKG_VARIANT_AUTO && p->variant != IKG_VARIANT_PAIR)
+    return fail(IKG_EINVAL, "variant %d not available in this build", p->variant);
+  return IKG_OK;
+}
+
+template <typename T>
+ikg::KParams<T> kparams(const ikg_params* p) {
+  ikg::KParams<T> k;
+  k.eps = (T)p->eps;
+  k.dt = (T)p->dt;
+  k.lambda = (T)p->lambda;
+  k.max_iters = p->max_iters;
+  return k;
+}
+
+template <typename T>
+int solve_batch_t(ikg_model* model, int device, const void* targets, const void* q0, int64_t q0_stride, int64_t B,
+                  const ikg_params* params, void* q_out, uint8_t* converged, int32_t* iters, void* err_out,
+                  hipStream_t s, uint32_t flags) {
+  const ikg::KModel<T>* dm = nullptr;
+  int rc = model->device_tables<T>(device, &dm);
+  if (rc) return rc;
+  const int nq = model->desc.nq;
+  ikg::BatchArgs a{targets, q0, q0_stride, B, q_out, converged, iters, err_out};
+  Staging st(s);
+  const bool host = flags & IKG_FLAG_HOST_POINTERS;
+  if (host) {
+    const int64_t q0_rows = q0_stride == 0 ? 1 : B;
+    a.targets = st.in(targets, sizeof(T) * 12 * B);
+    a.q0 = st.in(q0, sizeof(T) * (q0_stride == 0 ? nq : q0_stride * (q0_rows - 1) + nq));
+    a.q_out = st.out(sizeof(T) * nq * B);
+    a.converged = converged ? (uint8_t*)st.out(B) : nullptr;
+    a.iters = iters ? (int32_t*)st.out(sizeof(int32_t) * B) : nullptr;
+    a.err_out = err_out ? st.out(sizeof(T) * 2 * B) : nullptr;
+    if (st.rc) return st.rc;
+  }
+  hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, s);
+  if (e != hipSuccess) return hip_fail(e, "ikg pair kernel launch");
+  if (host) {
+    st.back(q_out, a.q_out, sizeof(T) * nq * B);
+    st.back(converged, a.converged, B);
+    st.back(iters, a.iters, sizeof(int32_t) * B);
+    st.back(err_out, a.err_out, sizeof(T) * 2 * B);
+    if (st.rc) return st.rc;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
+  return IKG_OK;
+}
+
+template <typename T>
+int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_, const void* seeds, int64_t S,
+                  const ikg_params* params, void* q_out, uint8_t* converged, int32_t* iters, void* err_out,
+                  int32_t* best_seed, hipStream_t s, uint32_t flags) {
+  const ikg::KModel<T>* dm = nullptr;
+  int rc = model->device_tables<T>(device, &dm);
+  if (rc) return rc;
+  const int nq = model->desc.nq;
+  ikg::MultiArgs a{targets, T_, seeds, S, q_out, converged, iters, err_out, best_seed};
+  Staging st(s);
+  const bool host = flags & IKG_FLAG_HOST_POINTERS;
+  if (host) {
+    a.targets = st.in(targets, sizeof(T) * 12 * T_);
+    a.seeds = st.in(seeds, sizeof(T) * nq * S);
+    a.q_out = st.out(sizeof(T) * nq * T_);
+    a.converged = converged ? (uint8_t*)st.out(T_) : nullptr;
+    a.iters = iters ? (int32_t*)st.out(sizeof(int32_t) * T_) : nullptr;
+    a.err_out = err_out ? st.out(sizeof(T) * 2 * T_) : nullptr;
+    a.best_seed = best_seed ? (int32_t*)st.out(sizeof(int32_t) * T_) : nullptr;
+    if (st.rc) return st.rc;
+  }
+  hipError_t e = ikg::launch_multistart<T>(dm, kparams<T>(params), a, s);
+  if (e != hipSuccess) return hip_fail(e, "ikg multistart kernel launch");
+  if (host) {
+    st.back(q_out, a.q_out, sizeof(T) * nq * T_);
+    st.back(converged, a.converged, T_);
+    st.back(iters, a.iters, sizeof(int32_t) * T_);
+    st.back(err_out, a.err_out, sizeof(T) * 2 * T_);
+    st.back(best_seed, a.best_seed, sizeof(int32_t) * T_);
+    if (st.rc) return st.rc;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
+  return IKG_OK;
+}
+
+template <typename T>
+int fk_t(ikg_model* model, int device, const void* q, int64_t B, void* hands, hipStream_t s, uint32_t flags) {
+  const ikg::KModel<T>* dm = nullptr;
+  int rc = model->device_tables<T>(device, &dm);
+  if (rc) return rc;
+  const int nq = model->desc.nq;
+  Staging st(s);
+  const bool host = flags & IKG_FLAG_HOST_POINTERS;
+  const void* dq = q;
+  void* dh = hands;
+  if (host) {
+    dq = st.in(q, sizeof(T) * nq * B);
+    dh = st.out(sizeof(T) * 24 * B);
+    if (st.rc) return st.rc;
+  }
+  hipError_t e = ikg::launch_fk<T>(dm, dq, B, dh, s);
+  if (e != hipSuccess) return hip_fail(e, "ikg fk kernel launch");
+  if (host) {
+    st.back(hands, dh, sizeof(T) * 24 * B);
+    if (st.rc) return st.rc;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
+  return IKG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ikg_last_error(void) { return g_err; }
+
+const char* ikg_version(void) { return "ikgrasp 0.1.0 (gfx950, pair kernel)"; }
+
+void ikg_params_default(ikg_params* p) {
+  if (!p) return;
+  p->eps = 1e-3;       // config.py:22
+  p->dt = 1e-2;        // inverse_geometry.py:54
+  p->max_iters = 1000;  // inverse_geometry.py:53
+  p->variant = IKG_VARIANT_AUTO;
+  p->lambda = 0.0;      // np.linalg.pinv semantics
+}
+
+int ikg_model_create(const ikg_model_desc* d, ikg_model** out) {
+  g_err[0] = 0;
+  if (!d || !out) return fail(IKG_EINVAL, "NULL argument");
+  *out = nullptr;
+  if (d->nq <= 0 || d->nq > IKG_MAX_NQ) return fail(IKG_EINVAL, "nq=%d outside [1,%d]", d->nq, IKG_MAX_NQ);
+  for (int q = 0; q < d->nq; ++q) {
+    if (d->axis[q] < 0 || d->axis[q] > 2) return fail(IKG_EINVAL, "joint %d: axis must be 0/1/2", q);
+    if (d->parent[q] < -1 || d->parent[q] >= q)
+      return fail(IKG_EINVAL, "joint %d: parent %d must precede it (Pinocchio order)", q, d->parent[q]);
+    if (!(d->lower[q] <= d->upper[q])) return fail(IKG_EINVAL, "joint %d: lower > upper", q);
+  }
+  const int r = d->root_q;
+  if (r < 0 || r >= d->nq || d->parent[r] != -1) return fail(IKG_EINVAL, "root_q must be a joint under the universe");
+  bool used[IKG_MAX_NQ] = {};
+  used[r] = true;
+  for (int a = 0; a < 2; ++a) {
+    int prev = r;
+    for (int j = 0; j < IKG_ARM_DOF; ++j) {
+      const int q = d->arm_q[a][j];
+      if (q < 0 || q >= d->nq || used[q]) return fail(IKG_EINVAL, "arm %d joint %d: bad or repeated q index", a, j);
+      if (d->parent[q] != prev) return fail(IKG_EINVAL, "arm %d joint %d: not a serial chain from the root", a, j);
+      used[q] = true;
+      prev = q;
+    }
+  }
+  for (int j = 0; j < IKG_ARM_DOF; ++j)
+    if (d->axis[d->arm_q[0][j]] != d->axis[d->arm_q[1][j]])
+      return fail(IKG_EINVAL, "arm joint %d: left/right axes differ (unsupported)", j);
+  if (!is_identity(d->placement[r])) {
+    // the root rotation is applied through rotate_axis(root_R): any rotation works
+  }
+  ikg_model* m = new (std::nothrow) ikg_model();
+  if (!m) return fail(IKG_ENOMEM, "out of host memory");
+  m->desc = *d;
+  build_kmodel<double>(*d, m->k64);
+  build_kmodel<float>(*d, m->k32);
+  *out = m;
+  return IKG_OK;
+}
+
+void ikg_model_destroy(ikg_model* m) {
+  if (!m) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  for (size_t i = 0; i < m->dev64.size(); ++i)
+    if (m->dev64[i]) {
+      (void)hipSetDevice((int)i);
+      (void)hipFree(m->dev64[i]);
+    }
+  for (size_t i = 0; i < m->dev32.size(); ++i)
+    if (m->dev32[i]) {
+      (void)hipSetDevice((int)i);
+      (void)hipFree(m->dev32[i]);
+    }
+  if (prev >= 0) (void)hipSetDevice(prev);
+  delete m;
+}
+
+int ikg_solve_batch(const ikg_model* model, int device, int dtype, const void* targets, const void* q0,
+                    int64_t q0_stride, int64_t B, const ikg_params* params, void* q_out, uint8_t* converged,
+                    int32_t* iters, void* err_out, void* stream, uint32_t flags) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (B < 0) return fail(IKG_EINVAL, "B must be >= 0");
+  if (B > 0 && (!targets || !q0 || !q_out)) return fail(IKG_EINVAL, "targets, q0 and q_out are required");
+  if (q0_stride != 0 && q0_stride < model->desc.nq) return fail(IKG_EINVAL, "q0_stride must be 0 or >= nq");
+  if (int rc = check_params(params)) return rc;
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  if (B == 0) return IKG_OK;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == IKG_F64 ? solve_batch_t<double>(m, device, targets, q0, q0_stride, B, params, q_out, converged,
+                                                  iters, err_out, s, flags)
+                          : solve_batch_t<float>(m, device, targets, q0, q0_stride, B, params, q_out, converged,
+                                                 iters, err_out, s, flags);
+}
+
+int ikg_solve_multistart(const ikg_model* model, int device, int dtype, const void* targets, int64_t T,
+                         const void* seeds, int64_t S, const ikg_params* params, void* q_out, uint8_t* converged,
+                         int32_t* iters, void* err_out, int32_t* best_seed, void* stream, uint32_t flags) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (T < 0 || S <= 0) return fail(IKG_EINVAL, "need T >= 0 and S >= 1");
+  if (S > ikg::kMaxSeedsPerBlock) return fail(IKG_EINVAL, "S=%lld seeds > %d per target", (long long)S, ikg::kMaxSeedsPerBlock);
+  if (T > 0 && (!targets || !seeds || !q_out)) return fail(IKG_EINVAL, "targets, seeds and q_out are required");
+  if (int rc = check_params(params)) return rc;
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  if (T == 0) return IKG_OK;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == IKG_F64 ? solve_multi_t<double>(m, device, targets, T, seeds, S, params, q_out, converged, iters,
+                                                  err_out, best_seed, s, flags)
+                          : solve_multi_t<float>(m, device, targets, T, seeds, S, params, q_out, converged, iters,
+                                                 err_out, best_seed, s, flags);
+}
+
+int ikg_fk_batch(const ikg_model* model, int device, int dtype, const void* q, int64_t B, void* hands, void* stream,
+                 uint32_t flags) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (B < 0) return fail(IKG_EINVAL, "B must be >= 0");
+  if (B > 0 && (!q || !hands)) return fail(IKG_EINVAL, "q and hands are required");
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  if (B == 0) return IKG_OK;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == IKG_F64 ? fk_t<double>(m, device, q, B, hands, s, flags)
+                          : fk_t<float>(m, device, q, B, hands, s, flags);
+}
+
+}  // extern "C"

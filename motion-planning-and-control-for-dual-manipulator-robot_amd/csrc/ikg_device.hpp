@@ -1,0 +1,405 @@
+// Device-side math for the batched grasp-pose IK (gfx950 / CDNA4).
+//
+// Every function here restates one piece of the reference loop
+// (/root/reference/inverse_geometry.py:56-94) or of the Pinocchio calls it
+// makes; the oracle (oracle/ik_oracle.py) is the independent CPU statement of
+// the same algorithm and is never linked into this library.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ikg {
+
+constexpr int kArmDof = 6;
+constexpr int kMaxNq = 32;
+
+// Kernel-side model tables (built once per model/dtype in ikg_capi.hip and
+// uploaded to device global memory; read through uniform scalar loads).
+template <typename T>
+struct KModel {
+  T root_R[9];
+  T root_t[3];
+  T root_lo, root_hi;
+  T arm_R[2][kArmDof][9];
+  T arm_t[2][kArmDof][3];
+  T arm_lo[2][kArmDof];
+  T arm_hi[2][kArmDof];
+  T hand_R[2][9];
+  T hand_t[2][3];
+  T hook_R[2][9];
+  T hook_t[2][3];
+  T lo[kMaxNq];
+  T hi[kMaxNq];
+  int32_t arm_q[2][kArmDof];
+  int32_t passive_q[kMaxNq];
+  int32_t n_passive;
+  int32_t root_q;
+  int32_t root_axis;
+  int32_t arm_axis[kArmDof];
+  int32_t nq;
+  int32_t rot_mask;  // bit k (k<6): arm joint k placement rotation != I; bit 6: root
+};
+
+template <typename T>
+struct KParams {
+  T eps;
+  T dt;
+  T lambda;
+  int32_t max_iters;
+};
+
+// ---------------------------------------------------------------- precision traits
+template <typename T>
+struct Prec;
+
+template <>
+struct Prec<double> {
+  // TaylorSeriesExpansion<double>::precision<3>() = eps^(1/4) (Pinocchio log3/log6)
+  static constexpr double kPrec3 = 1.220703125e-04;
+  static constexpr double kPi = 3.14159265358979323846;
+  // relative cut-off for the triangular solve (np.linalg.pinv rcond = 1e-15)
+  static constexpr double kRcond = 1e-15;
+  __device__ static inline void sincos_(double x, double* s, double* c) { ::sincos(x, s, c); }
+};
+
+template <>
+struct Prec<float> {
+  // fp32 kernel: series branches widened so the float path tracks the fp64
+  // reference ("fp32 numerics"); 0.1 keeps the truncated series
+  // below 1e-13 relative.
+  static constexpr float kPrec3 = 0.1f;
+  static constexpr float kPi = 3.14159265358979323846f;
+  static constexpr float kRcond = 1e-7f;
+  __device__ static inline void sincos_(float x, float* s, float* c) { ::sincosf(x, s, c); }
+};
+
+template <typename T>
+__device__ inline T sel(bool b, T x, T y) { return b ? x : y; }
+
+// ---------------------------------------------------------------- cross-lane
+// Exchange a value with the partner lane (lane ^ 1) through a DPP quad_perm
+// [1,0,3,2]: no LDS traffic, one VALU op per dword.
+__device__ inline int pair_swap_i32(int x) {
+  return __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false);
+}
+__device__ inline float pair_swap(float x) {
+  return __int_as_float(pair_swap_i32(__float_as_int(x)));
+}
+__device__ inline double pair_swap(double x) {
+  int lo = __double2loint(x), hi = __double2hiint(x);
+  lo = pair_swap_i32(lo);
+  hi = pair_swap_i32(hi);
+  return __hiloint2double(hi, lo);
+}
+
+// ---------------------------------------------------------------- SE(3) pieces
+// R is row-major: R[3*r + c].
+template <typename T>
+__device__ inline void matmul3(const T* A, const T* B, T* C) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      C[3 * r + c] = A[3 * r + 0] * B[0 + c] + A[3 * r + 1] * B[3 + c] + A[3 * r + 2] * B[6 + c];
+}
+
+// C = A^T B
+template <typename T>
+__device__ inline void matmul3_tn(const T* A, const T* B, T* C) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      C[3 * r + c] = A[0 + r] * B[0 + c] + A[3 + r] * B[3 + c] + A[6 + r] * B[6 + c];
+}
+
+template <typename T>
+__device__ inline void matvec3(const T* A, const T* x, T* y) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) y[r] = A[3 * r] * x[0] + A[3 * r + 1] * x[1] + A[3 * r + 2] * x[2];
+}
+
+template <typename T>
+__device__ inline void matvec3_t(const T* A, const T* x, T* y) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) y[r] = A[r] * x[0] + A[3 + r] * x[1] + A[6 + r] * x[2];
+}
+
+// R <- R * Rot_axis(q) given (s, c) = sincos(q): JointModelR{X,Y,Z}::calc
+// composed onto the parent rotation (only two columns change).
+template <typename T>
+__device__ inline void rotate_axis(T* R, int axis, T s, T c) {
+  if (axis == 0) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      T c1 = R[3 * r + 1], c2 = R[3 * r + 2];
+      R[3 * r + 1] = c * c1 + s * c2;
+      R[3 * r + 2] = c * c2 - s * c1;
+    }
+  } else if (axis == 1) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      T c0 = R[3 * r + 0], c2 = R[3 * r + 2];
+      R[3 * r + 0] = c * c0 - s * c2;
+      R[3 * r + 2] = c * c2 + s * c0;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      T c0 = R[3 * r + 0], c1 = R[3 * r + 1];
+      R[3 * r + 0] = c * c0 + s * c1;
+      R[3 * r + 1] = c * c1 - s * c0;
+    }
+  }
+}
+
+template <typename T>
+__device__ inline void column(const T* R, int axis, T* a) {
+  a[0] = axis == 0 ? R[0] : (axis == 1 ? R[1] : R[2]);
+  a[1] = axis == 0 ? R[3] : (axis == 1 ? R[4] : R[5]);
+  a[2] = axis == 0 ? R[6] : (axis == 1 ? R[7] : R[8]);
+}
+
+// ---------------------------------------------------------------- log3 / log6
+// pin.log3 (2.6-era branch structure) and pin.log6 ->
+// [v; w] (inverse_geometry.py:66-67).
+template <typename T>
+__device__ inline void log6(const T* R, const T* p, T* e) {
+  const T pi = Prec<T>::kPi;
+  const T tr = R[0] + R[4] + R[8];
+  const T sx = R[7] - R[5], sy = R[2] - R[6], sz = R[3] - R[1];
+  T theta;
+  if constexpr (sizeof(T) == 8) {
+    theta = tr > T(3) ? T(0) : (tr < T(-1) ? pi : acos((tr - T(1)) / T(2)));
+  } else {
+    // fp32: atan2 of (sin, cos) keeps theta accurate near 0 where acos is not.
+    const T sn = sqrtf(sx * sx + sy * sy + sz * sz) * T(0.5);
+    theta = atan2f(sn, (tr - T(1)) * T(0.5));
+  }
+  T w[3];
+  if (theta >= pi - T(1e-2)) {
+    T s_, cphi;
+    Prec<T>::sincos_(theta - pi, &s_, &cphi);
+    const T beta = theta * theta / (T(1) + cphi);
+    const T t0 = (R[0] + cphi) * beta, t1 = (R[4] + cphi) * beta, t2 = (R[8] + cphi) * beta;
+    w[0] = (R[7] > R[5] ? T(1) : T(-1)) * (t0 > T(0) ? sqrt(t0) : T(0));
+    w[1] = (R[2] > R[6] ? T(1) : T(-1)) * (t1 > T(0) ? sqrt(t1) : T(0));
+    w[2] = (R[3] > R[1] ? T(1) : T(-1)) * (t2 > T(0) ? sqrt(t2) : T(0));
+  } else {
+    T f;
+    if (theta > Prec<T>::kPrec3) {
+      f = theta / sin(theta);
+    } else if constexpr (sizeof(T) == 8) {
+      f = T(1);  // Pinocchio: theta/sin(theta) -> 1 below precision<3>()
+    } else {
+      const T t2 = theta * theta;
+      f = T(1) + t2 * (T(1) / T(6) + t2 * (T(7) / T(360)));
+    }
+    f *= T(0.5);
+    w[0] = f * sx;
+    w[1] = f * sy;
+    w[2] = f * sz;
+  }
+  T alpha, beta;
+  const T t2 = theta * theta;
+  if (theta < Prec<T>::kPrec3) {
+    if constexpr (sizeof(T) == 8) {
+      alpha = T(1) - t2 / T(12) - t2 * t2 / T(720);
+      beta = T(1) / T(12) + t2 / T(720);
+    } else {
+      alpha = T(1) - t2 * (T(1) / T(12) + t2 * (T(1) / T(720) + t2 * (T(1) / T(30240))));
+      beta = T(1) / T(12) + t2 * (T(1) / T(720) + t2 * (T(1) / T(30240) + t2 * (T(1) / T(1209600))));
+    }
+  } else {
+    if constexpr (sizeof(T) == 8) {
+      T st, ct;
+      Prec<T>::sincos_(theta, &st, &ct);
+      alpha = theta * st / (T(2) * (T(1) - ct));
+      beta = T(1) / t2 - st / (T(2) * theta * (T(1) - ct));
+    } else {
+      // half-angle form: no 1-cos cancellation in fp32
+      T sh, ch;
+      Prec<T>::sincos_(theta * T(0.5), &sh, &ch);
+      alpha = theta * T(0.5) * ch / sh;
+      beta = (T(1) - alpha) / t2;
+    }
+  }
+  const T wp = w[0] * p[0] + w[1] * p[1] + w[2] * p[2];
+  const T bwp = beta * wp;
+  // v = alpha p - 0.5 w x p + (beta w.p) w
+  e[0] = alpha * p[0] - T(0.5) * (w[1] * p[2] - w[2] * p[1]) + bwp * w[0];
+  e[1] = alpha * p[1] - T(0.5) * (w[2] * p[0] - w[0] * p[2]) + bwp * w[1];
+  e[2] = alpha * p[2] - T(0.5) * (w[0] * p[1] - w[1] * p[0]) + bwp * w[2];
+  e[3] = w[0];
+  e[4] = w[1];
+  e[5] = w[2];
+}
+
+// ---------------------------------------------------------------- one arm's kinematics
+// Forward kinematics of the shared root joint + one arm (pin.forwardKinematics
+// restricted to the hand's support, inverse_geometry.py:58) producing:
+//   Rh, th  : effector frame placement oMf (data.oMf[LARM/RARM_EFF], :62-63)
+//   ax, org : world axis / origin of the 7 supporting joints (root first)
+template <typename T, bool WANT_AXES>
+__device__ inline void fk_arm(const KModel<T>* __restrict__ m, int arm, T qc, const T* qa, T* Rh, T* th,
+                              T (*ax)[3], T (*org)[3]) {
+  T R[9], t[3];
+  T s, c;
+  Prec<T>::sincos_(qc, &s, &c);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = m->root_R[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = m->root_t[i];
+  rotate_axis(R, m->root_axis, s, c);
+  if constexpr (WANT_AXES) {
+    column(R, m->root_axis, ax[0]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) org[0][i] = t[i];
+  }
+  const bool right = arm != 0;
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) {
+    T pt[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) pt[i] = sel(right, m->arm_t[1][k][i], m->arm_t[0][k][i]);
+    T dt_[3];
+    matvec3(R, pt, dt_);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t[i] += dt_[i];
+    if (m->rot_mask & (1 << k)) {
+      T P[9], Rn[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) P[i] = sel(right, m->arm_R[1][k][i], m->arm_R[0][k][i]);
+      matmul3(R, P, Rn);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+    }
+    Prec<T>::sincos_(qa[k], &s, &c);
+    const int axis = m->arm_axis[k];
+    rotate_axis(R, axis, s, c);
+    if constexpr (WANT_AXES) {
+      column(R, axis, ax[k + 1]);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) org[k + 1][i] = t[i];
+    }
+  }
+  T ht[3], hR[9], d[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ht[i] = sel(right, m->hand_t[1][i], m->hand_t[0][i]);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) hR[i] = sel(right, m->hand_R[1][i], m->hand_R[0][i]);
+  matvec3(R, ht, d);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) th[i] = t[i] + d[i];
+  matmul3(R, hR, Rh);
+}
+
+// log6(oMhand^-1 * oMtarget) (inverse_geometry.py:66-67)
+template <typename T>
+__device__ inline void pose_error(const T* Rh, const T* th, const T* RT, const T* tT, T* e) {
+  T Rm[9], d[3], pm[3];
+  matmul3_tn(Rh, RT, Rm);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d[i] = tT[i] - th[i];
+  matvec3_t(Rh, d, pm);
+  log6(Rm, pm, e);
+}
+
+// ---------------------------------------------------------------- 6x6 solve, 2 RHS
+// Householder QR of the square arm Jacobian A[:, 0:6] applied to the two
+// right-hand sides A[:, 6] (error) and A[:, 7] (root column); returns
+// x = A^-1 b for both.  Diagonal entries below rcond * max|R_kk| are
+// truncated to a zero inverse (the analogue of pinv's rcond).
+template <typename T>
+__device__ inline void qr_solve6(T (&A)[6][8], T* x0, T* x1) {
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    T n2 = T(0);
+#pragma unroll
+    for (int i = k; i < 6; ++i) n2 += A[i][k] * A[i][k];
+    const T nrm = sqrt(n2);
+    const T akk = A[k][k];
+    const T alpha = akk >= T(0) ? -nrm : nrm;
+    const T vk = akk - alpha;
+    const T vtv = T(2) * nrm * (nrm + fabs(akk));
+    const T scale = vtv > T(0) ? T(2) / vtv : T(0);
+#pragma unroll
+    for (int j = k + 1; j < 8; ++j) {
+      T tau = vk * A[k][j];
+#pragma unroll
+      for (int i = k + 1; i < 6; ++i) tau += A[i][k] * A[i][j];
+      const T f = tau * scale;
+      A[k][j] -= f * vk;
+#pragma unroll
+      for (int i = k + 1; i < 6; ++i) A[i][j] -= f * A[i][k];
+    }
+    A[k][k] = alpha;
+  }
+  T dmax = T(0);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dmax = fmax(dmax, fabs(A[k][k]));
+  const T cut = dmax * Prec<T>::kRcond;
+  T rd[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) rd[k] = fabs(A[k][k]) > cut ? T(1) / A[k][k] : T(0);
+#pragma unroll
+  for (int r = 5; r >= 0; --r) {
+    T s0 = A[r][6], s1 = A[r][7];
+#pragma unroll
+    for (int j = r + 1; j < 6; ++j) {
+      s0 -= A[r][j] * x0[j];
+      s1 -= A[r][j] * x1[j];
+    }
+    x0[r] = s0 * rd[r];
+    x1[r] = s1 * rd[r];
+  }
+}
+
+// Cholesky solve of the damped arm block (J_a J_a^T + lambda I) for 2 RHS.
+template <typename T>
+__device__ inline void chol_solve6(T (&M)[6][6], T* b0, T* b1) {
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    T d = M[k][k];
+#pragma unroll
+    for (int j = 0; j < k; ++j) d -= M[k][j] * M[k][j];
+    const T r = d > T(0) ? T(1) / sqrt(d) : T(0);
+    M[k][k] = r;  // store the reciprocal of L_kk
+#pragma unroll
+    for (int i = k + 1; i < 6; ++i) {
+      T v = M[i][k];
+#pragma unroll
+      for (int j = 0; j < k; ++j) v -= M[i][j] * M[k][j];
+      M[i][k] = v * r;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      b0[i] -= M[i][j] * b0[j];
+      b1[i] -= M[i][j] * b1[j];
+    }
+    b0[i] *= M[i][i];
+    b1[i] *= M[i][i];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+#pragma unroll
+    for (int j = i + 1; j < 6; ++j) {
+      b0[i] -= M[j][i] * b0[j];
+      b1[i] -= M[j][i] * b1[j];
+    }
+    b0[i] *= M[i][i];
+    b1[i] *= M[i][i];
+  }
+}
+
+template <typename T>
+__device__ inline T clampq(T q, T lo, T hi) {
+  // np.minimum(np.maximum(lower, q), upper)  (tools.py:21-22)
+  return fmin(fmax(lo, q), hi);
+}
+
+}  // namespace ikg

@@ -1,0 +1,358 @@
+// Batched dual-arm grasp-pose IK kernels for MI355X (gfx950).
+//
+// Hot path replaced: the iteration loop of computeqgrasppose
+// (/root/reference/inverse_geometry.py:56-94):
+//   FK (:58) -> 2x log6 error (:66-67) -> stop test (:70) -> 2x LOCAL frame
+//   Jacobian (:75-76) -> pinv(J) e (:83) -> integrate (:86) -> clamp (:89).
+//
+// Layout ("pair" variant): two lanes per IK problem, one per arm.  Lane 2p
+// owns the left arm of problem p, lane 2p+1 the right arm; both carry the
+// shared chest joint.  The 12x13 minimum-norm solve
+//     dq = J^T (J J^T)^-1 e
+// is split by the block structure J = [c | blockdiag(J_L, J_R)] (c = chest
+// column): each lane solves its square 6x6 arm system for two right-hand
+// sides (u = J_a^-1 e_a, v = J_a^-1 c_a) and the lanes exchange two scalars
+// through DPP to form the Sherman–Morrison chest step
+//     s = (u_L.v_L + u_R.v_R) / (1 + |v_L|^2 + |v_R|^2),  dq_c = s,
+//     dq_a = u_a - s v_a,
+// which equals pinv(J) e whenever J has full row rank.
+// No LDS, no barriers; the model tables are read with uniform scalar loads.
+#include <hip/hip_runtime.h>
+
+#include "ikg_device.hpp"
+#include "ikg_launch.hpp"
+
+namespace ikg {
+
+// One problem, one arm: run the reference loop to its stop condition.
+// Returns (through refs) the final q of this lane, the update count and the
+// norm of this lane's hand error at the returned q.
+template <typename T, bool DAMPED>
+__device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, const T* RT,
+                                  const T* tT, T& qc, T* qa, int& it_out, bool& conv_out, T& nrm_out,
+                                  T& other_out) {
+  const bool right = arm != 0;
+  const T root_lo = m->root_lo, root_hi = m->root_hi;
+  int it = 0;
+  bool conv = false;
+  T nrm, other;
+  for (;;) {
+    T Rh[9], th[3], ax[7][3], org[7][3];
+    fk_arm<T, true>(m, arm, qc, qa, Rh, th, ax, org);
+    T e[6];
+    pose_error(Rh, th, RT, tT, e);
+    nrm = sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3] + e[4] * e[4] + e[5] * e[5]);
+    other = pair_swap(nrm);
+    if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
+    if (nrm < prm.eps && other < prm.eps) {
+      conv = true;
+      break;
+    }
+    // World-aligned Jacobian at the hand point: col_j = [a_j x (p_h - o_j); a_j].
+    // LOCAL = blockdiag(Rh^T, Rh^T) * world-aligned, so solving with the
+    // rotated error Rh e gives the same dq (the rotation is orthogonal).
+    T A[6][8];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const int col = j == 0 ? 7 : j - 1;
+      const T dx = th[0] - org[j][0], dy = th[1] - org[j][1], dz = th[2] - org[j][2];
+      A[0][col] = ax[j][1] * dz - ax[j][2] * dy;
+      A[1][col] = ax[j][2] * dx - ax[j][0] * dz;
+      A[2][col] = ax[j][0] * dy - ax[j][1] * dx;
+      A[3][col] = ax[j][0];
+      A[4][col] = ax[j][1];
+      A[5][col] = ax[j][2];
+    }
+    T ev[3], ew[3];
+    matvec3(Rh, e, ev);
+    matvec3(Rh, e + 3, ew);
+    A[0][6] = ev[0];
+    A[1][6] = ev[1];
+    A[2][6] = ev[2];
+    A[3][6] = ew[0];
+    A[4][6] = ew[1];
+    A[5][6] = ew[2];
+
+    T dq[6], s;
+    if constexpr (!DAMPED) {
+      T u[6], v[6];
+      qr_solve6(A, u, v);
+      T alpha = T(0), beta = T(0);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        alpha += u[k] * v[k];
+        beta += v[k] * v[k];
+      }
+      const T at = alpha + pair_swap(alpha);
+      const T bt = beta + pair_swap(beta);
+      s = at / (T(1) + bt);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) dq[k] = u[k] - s * v[k];
+    } else {
+      // (J J^T + lambda I) y = e with J J^T = blockdiag(J_L J_L^T, J_R J_R^T) + c c^T
+      T M[6][6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c <= r; ++c) {
+          T acc = r == c ? prm.lambda : T(0);
+#pragma unroll
+          for (int k = 0; k < 6; ++k) acc += A[r][k] * A[c][k];
+          M[r][c] = acc;
+        }
+      T ze[6], zc[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        ze[r] = A[r][6];
+        zc[r] = A[r][7];
+      }
+      chol_solve6(M, ze, zc);
+      T alpha = T(0), beta = T(0);
+#pragma unroll
+      for (int r = 0; r < 6; ++r) {
+        alpha += A[r][7] * ze[r];
+        beta += A[r][7] * zc[r];
+      }
+      const T at = alpha + pair_swap(alpha);
+      const T bt = beta + pair_swap(beta);
+      s = at / (T(1) + bt);
+      T y[6];
+#pragma unroll
+      for (int r = 0; r < 6; ++r) y[r] = ze[r] - s * zc[r];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) {
+        T acc = T(0);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) acc += A[r][k] * y[r];
+        dq[k] = acc;
+      }
+    }
+    // pin.integrate (q + dq * DT) then projecttojointlimits
+    qc = clampq(qc + s * prm.dt, root_lo, root_hi);
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) {
+      const T lo = sel(right, m->arm_lo[1][k], m->arm_lo[0][k]);
+      const T hi = sel(right, m->arm_hi[1][k], m->arm_hi[0][k]);
+      qa[k] = clampq(qa[k] + dq[k] * prm.dt, lo, hi);
+    }
+    ++it;
+  }
+  it_out = it;
+  conv_out = conv;
+  nrm_out = nrm;
+  other_out = other;
+}
+
+// tools.getcubeplacement: oMcube * hook (tools.py:54-59), for this lane's arm.
+template <typename T>
+__device__ inline void hook_target(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ tg, T* RT,
+                                   T* tT) {
+  const bool right = arm != 0;
+  T CR[9], Ct[3], HR[9], Ht[3], d[3];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) CR[i] = tg[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) Ct[i] = tg[9 + i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) HR[i] = sel(right, m->hook_R[1][i], m->hook_R[0][i]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) Ht[i] = sel(right, m->hook_t[1][i], m->hook_t[0][i]);
+  matmul3(CR, HR, RT);
+  matvec3(CR, Ht, d);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) tT[i] = Ct[i] + d[i];
+}
+
+template <typename T>
+__device__ inline void load_q(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow, T& qc, T* qa) {
+  qc = qrow[m->root_q];
+  const bool right = arm != 0;
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) qa[k] = qrow[right ? m->arm_q[1][k] : m->arm_q[0][k]];
+}
+
+template <typename T>
+__device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow, int it, T qc,
+                               const T* qa, T* __restrict__ qo) {
+  const bool right = arm != 0;
+  if (!right) {
+    qo[m->root_q] = qc;
+    // passive joints (HEAD_JOINT0/1): zero Jacobian columns, so only the clamp
+    // of the first update moves them (tools.py:21-22)
+    for (int i = 0; i < m->n_passive; ++i) {
+      const int j = m->passive_q[i];
+      const T v = qrow[j];
+      qo[j] = it > 0 ? clampq(v, m->lo[j], m->hi[j]) : v;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) qo[right ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
+}
+
+template <typename T, bool DAMPED>
+__global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
+                                                            const T* __restrict__ targets,
+                                                            const T* __restrict__ q0, int64_t q0_stride, int64_t B,
+                                                            T* __restrict__ q_out, uint8_t* __restrict__ conv_out,
+                                                            int32_t* __restrict__ iters_out,
+                                                            T* __restrict__ err_out) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = gid >> 1;
+  const int arm = (int)(gid & 1);
+  if (p >= B) return;  // both lanes of a pair leave together
+  T RT[9], tT[3];
+  hook_target(m, arm, targets + p * 12, RT, tT);
+  const T* qrow = q0 + p * q0_stride;
+  T qc, qa[kArmDof];
+  load_q(m, arm, qrow, qc, qa);
+  int it;
+  bool conv;
+  T nrm, other;
+  solve_pair<T, DAMPED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
+  store_q(m, arm, qrow, it, qc, qa, q_out + p * m->nq);
+  if (arm == 0) {
+    if (conv_out) conv_out[p] = conv ? 1 : 0;
+    if (iters_out) iters_out[p] = it;
+  }
+  if (err_out) err_out[p * 2 + arm] = nrm;
+}
+
+// Multi-start: one workgroup per target, seed i on lanes (2i, 2i+1); the
+// best seed is reduced in LDS inside the workgroup (no cross-GPU traffic).
+template <typename T, bool DAMPED>
+__global__ __launch_bounds__(1024) void ikg_multistart_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
+                                                              const T* __restrict__ targets,
+                                                              const T* __restrict__ seeds, int64_t S,
+                                                              T* __restrict__ q_out, uint8_t* __restrict__ conv_out,
+                                                              int32_t* __restrict__ iters_out,
+                                                              T* __restrict__ err_out,
+                                                              int32_t* __restrict__ best_out) {
+  __shared__ T s_key[kMaxSeedsPerBlock];
+  __shared__ int s_idx[kMaxSeedsPerBlock];
+  const int64_t tgt = blockIdx.x;
+  const int seed = threadIdx.x >> 1;
+  const int arm = threadIdx.x & 1;
+  const bool active = seed < S;
+  int n = 1;  // power-of-two reduction width covering every seed slot
+  while (n < (int)(blockDim.x >> 1)) n <<= 1;
+  if ((int)threadIdx.x < n) {
+    s_key[threadIdx.x] = T(3.0e38);
+    s_idx[threadIdx.x] = threadIdx.x;
+  }
+  T qc = T(0), qa[kArmDof] = {};
+  int it = 0;
+  bool conv = false;
+  T nrm = T(0), other = T(0);
+  const T* qrow = seeds + (int64_t)(active ? seed : 0) * m->nq;
+  if (active) {
+    T RT[9], tT[3];
+    hook_target(m, arm, targets + tgt * 12, RT, tT);
+    load_q(m, arm, qrow, qc, qa);
+    solve_pair<T, DAMPED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
+  }
+  __syncthreads();
+  // key: converged seeds rank by the worse hand error; unconverged ones after
+  // them (offset 1e30); ties resolve to the lower seed index.
+  if (arm == 0 && active) {
+    const T worst = fmax(nrm, other);
+    s_key[seed] = conv ? worst : T(1e30) + worst;
+  }
+  __syncthreads();
+  for (int stride = n / 2; stride > 0; stride >>= 1) {
+    const int i = threadIdx.x;
+    if (i < stride) {
+      const T ka = s_key[i], kb = s_key[i + stride];
+      const int ia = s_idx[i], ib = s_idx[i + stride];
+      if (kb < ka || (kb == ka && ib < ia)) {
+        s_key[i] = kb;
+        s_idx[i] = ib;
+      }
+    }
+    __syncthreads();
+  }
+  const int best = s_idx[0];
+  if (active && seed == best) {
+    store_q(m, arm, qrow, it, qc, qa, q_out + tgt * m->nq);
+    if (arm == 0) {
+      if (conv_out) conv_out[tgt] = conv ? 1 : 0;
+      if (iters_out) iters_out[tgt] = it;
+      if (best_out) best_out[tgt] = best;
+    }
+    if (err_out) err_out[tgt * 2 + arm] = nrm;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void ikg_fk_kernel(const KModel<T>* __restrict__ m, const T* __restrict__ q,
+                                                     int64_t B, T* __restrict__ hands) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= B) return;
+  const T* qrow = q + p * m->nq;
+#pragma unroll 1
+  for (int arm = 0; arm < 2; ++arm) {
+    T qc, qa[kArmDof], Rh[9], th[3];
+    load_q(m, arm, qrow, qc, qa);
+    fk_arm<T, false>(m, arm, qc, qa, Rh, th, nullptr, nullptr);
+    T* out = hands + p * 24 + arm * 12;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) out[i] = Rh[i];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) out[9 + i] = th[i];
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+template <typename T>
+hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
+  if (a.B <= 0) return hipSuccess;
+  constexpr int block = 64;
+  const int64_t threads = a.B * 2;
+  const dim3 grid((unsigned)((threads + block - 1) / block));
+  if (prm.lambda > T(0))
+    hipLaunchKernelGGL((ikg_pair_batch_kernel<T, true>), grid, dim3(block), 0, s, dmodel, prm,
+                       (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, (T*)a.q_out, a.converged, a.iters,
+                       (T*)a.err_out);
+  else
+    hipLaunchKernelGGL((ikg_pair_batch_kernel<T, false>), grid, dim3(block), 0, s, dmodel, prm,
+                       (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, (T*)a.q_out, a.converged, a.iters,
+                       (T*)a.err_out);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, hipStream_t s) {
+  if (a.T <= 0) return hipSuccess;
+  const int block = (int)(((a.S * 2) + 63) / 64 * 64);
+  const dim3 grid((unsigned)a.T);
+  if (prm.lambda > T(0))
+    hipLaunchKernelGGL((ikg_multistart_kernel<T, true>), grid, dim3(block), 0, s, dmodel, prm,
+                       (const T*)a.targets, (const T*)a.seeds, a.S, (T*)a.q_out, a.converged, a.iters,
+                       (T*)a.err_out, a.best_seed);
+  else
+    hipLaunchKernelGGL((ikg_multistart_kernel<T, false>), grid, dim3(block), 0, s, dmodel, prm,
+                       (const T*)a.targets, (const T*)a.seeds, a.S, (T*)a.q_out, a.converged, a.iters,
+                       (T*)a.err_out, a.best_seed);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_fk(const KModel<T>* dmodel, const void* q, int64_t B, void* hands, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  constexpr int block = 256;
+  const dim3 grid((unsigned)((B + block - 1) / block));
+  hipLaunchKernelGGL((ikg_fk_kernel<T>), grid, dim3(block), 0, s, dmodel, (const T*)q, B, (T*)hands);
+  return hipGetLastError();
+}
+
+template hipError_t launch_pair_batch<double>(const KModel<double>*, const KParams<double>&, const BatchArgs&,
+                                              hipStream_t);
+template hipError_t launch_pair_batch<float>(const KModel<float>*, const KParams<float>&, const BatchArgs&,
+                                             hipStream_t);
+template hipError_t launch_multistart<double>(const KModel<double>*, const KParams<double>&, const MultiArgs&,
+                                              hipStream_t);
+template hipError_t launch_multistart<float>(const KModel<float>*, const KParams<float>&, const MultiArgs&,
+                                             hipStream_t);
+template hipError_t launch_fk<double>(const KModel<double>*, const void*, int64_t, void*, hipStream_t);
+template hipError_t launch_fk<float>(const KModel<float>*, const void*, int64_t, void*, hipStream_t);
+
+}  // namespace ikg

@@ -1,0 +1,45 @@
+// Host-side launcher declarations shared by ikg_kernels.hip and ikg_capi.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ikg_device.hpp"
+
+namespace ikg {
+
+struct BatchArgs {
+  const void* targets;
+  const void* q0;
+  int64_t q0_stride;
+  int64_t B;
+  void* q_out;
+  uint8_t* converged;
+  int32_t* iters;
+  void* err_out;
+};
+
+struct MultiArgs {
+  const void* targets;
+  int64_t T;
+  const void* seeds;
+  int64_t S;
+  void* q_out;
+  uint8_t* converged;
+  int32_t* iters;
+  void* err_out;
+  int32_t* best_seed;
+};
+
+template <typename T>
+hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s);
+
+template <typename T>
+hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, hipStream_t s);
+
+template <typename T>
+hipError_t launch_fk(const KModel<T>* dmodel, const void* q, int64_t B, void* hands, hipStream_t s);
+
+constexpr int kMaxSeedsPerBlock = 512;
+
+}  // namespace ikg

@@ -1,0 +1,57 @@
+"""Drop-in `computeqgrasppose` (reference inverse_geometry.py:17-100) backed
+by the batched HIP kernel, plus the batched / multi-start APIs.
+
+    q, success = computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None)
+
+Same name, positional order and return as the reference.  Differences that
+a caller can observe:
+  * `success` is the convergence test of :70 only; the collision term
+    (tools.py:25-35) is the next scope row (§8f-1) and is not evaluated;
+  * `viz` is updated once with the final q instead of every iteration.
+`qcurrent` is copied, never mutated (:49); the cube is left placed at
+`cubetarget` (:42, tools.py:62-68).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .config import CUBE_PLACEMENT, CUBE_PLACEMENT_TARGET, EPSILON, DT_IK, MAX_ITERS  # noqa: F401
+from .se3 import as_rt, pack_targets
+from .tools import setcubeplacement
+
+
+def _solver_of(robot):
+    solver = getattr(robot, "solver", None)
+    if solver is None:
+        raise TypeError(f"robot of type {type(robot).__name__} carries no ikgrasp solver; "
+                        "build it with ikgrasp.scene.setuppinocchio()")
+    return solver
+
+
+def computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None):
+    """inverse_geometry.py:17 — returns (q float64[nq], success bool)."""
+    setcubeplacement(robot, cube, cubetarget)  # :42
+    R, t = as_rt(cubetarget)
+    target = np.concatenate([R.reshape(9), t])[None, :]
+    q0 = np.array(qcurrent, dtype=np.float64).copy()  # :49
+    sol = _solver_of(robot).solve(target, q0, dtype="f64", eps=EPSILON, dt=DT_IK, max_iters=MAX_ITERS)
+    q = sol.q[0].astype(np.float64)
+    if viz is not None and hasattr(viz, "display"):  # :92-94, once with the final q
+        viz.display(q)
+    return q, bool(sol.converged[0])
+
+
+def computeqgrasppose_batch(robot, qcurrent, cubetargets, dtype="f64", **kw):
+    """Batched API: cubetargets [B,12] / [B,4,4] / list of SE3; qcurrent [nq]
+    (broadcast) or [B,nq] -> (q [B,nq], success [B], iters [B])."""
+    targets = pack_targets(cubetargets)
+    sol = _solver_of(robot).solve(targets, np.asarray(qcurrent), dtype=dtype, **kw)
+    return sol.q, sol.converged, sol.iters
+
+
+def computeqgrasppose_multistart(robot, seeds, cubetargets, dtype="f64", **kw):
+    """Multi-start API: seeds [S,nq] x targets -> best seed per target:
+    (q [T,nq], success [T], best_seed [T])."""
+    targets = pack_targets(cubetargets)
+    sol = _solver_of(robot).solve_multistart(targets, np.asarray(seeds), dtype=dtype, **kw)
+    return sol.q, sol.converged, sol.best_seed

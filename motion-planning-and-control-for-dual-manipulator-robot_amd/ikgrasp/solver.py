@@ -1,0 +1,161 @@
+"""Batched solver front-end over the C-ABI.
+
+`IKSolver` accepts either numpy arrays (host memory: the library stages them
+through device scratch) or torch tensors already resident on a ROCm device
+(device pointers, launched on torch's current stream — the zero-copy path the
+benchmark uses).  The HIP kernel is the only compute path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .model import DualArmModel, load_nextage
+
+_DT = {"f64": (_lib.IKG_F64, np.float64), "f32": (_lib.IKG_F32, np.float32)}
+
+
+def _dtype(dtype):
+    if dtype in ("f64", "float64", np.float64, "double"):
+        return _DT["f64"]
+    if dtype in ("f32", "float32", np.float32, "float"):
+        return _DT["f32"]
+    try:
+        import torch
+        if dtype == torch.float64:
+            return _DT["f64"]
+        if dtype == torch.float32:
+            return _DT["f32"]
+    except ImportError:  # pragma: no cover
+        pass
+    raise ValueError(f"unsupported dtype {dtype!r}")
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+@dataclass
+class Solution:
+    q: object            # [B, nq]
+    converged: object    # [B] bool/uint8
+    iters: object        # [B] int32
+    err: object          # [B, 2] |log6| left/right at q
+    best_seed: object = None
+
+
+class IKSolver:
+    """Owns one native model (`ikg_model_create`)."""
+
+    def __init__(self, model: DualArmModel | None = None, device: int = 0):
+        self.lib = _lib.load()
+        self.model = model if model is not None else load_nextage()
+        self.desc = _lib.model_desc(self.model)
+        h = C.c_void_p()
+        _lib.check(self.lib.ikg_model_create(C.byref(self.desc), C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            self.lib.ikg_model_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def nq(self) -> int:
+        return self.model.nq
+
+    def params(self, eps=1e-3, dt=1e-2, max_iters=1000, lam=0.0, variant=_lib.IKG_VARIANT_AUTO):
+        return _lib.default_params(eps=eps, dt=dt, max_iters=max_iters, lambda_=lam, variant=variant)
+
+    # ------------------------------------------------------------------ batch
+    def solve(self, targets, q0, dtype="f64", stream=None, **kw) -> Solution:
+        """targets [B,12] cube placements; q0 [nq] (broadcast) or [B,nq]."""
+        prm = self.params(**kw)
+        if _is_torch(targets):
+            return self._solve_torch(targets, q0, prm, stream)
+        code, npt = _dtype(dtype)
+        tg = np.ascontiguousarray(targets, dtype=npt).reshape(-1, 12)
+        B = tg.shape[0]
+        q = np.ascontiguousarray(q0, dtype=npt)
+        stride = 0 if q.ndim == 1 else self.nq
+        if q.ndim == 2 and q.shape != (B, self.nq):
+            raise ValueError(f"q0 must be [{self.nq}] or [{B},{self.nq}], got {q.shape}")
+        if q.ndim == 1 and q.shape != (self.nq,):
+            raise ValueError(f"q0 must have {self.nq} entries")
+        q_out = np.empty((B, self.nq), dtype=npt)
+        conv = np.empty(B, dtype=np.uint8)
+        iters = np.empty(B, dtype=np.int32)
+        err = np.empty((B, 2), dtype=npt)
+        _lib.check(self.lib.ikg_solve_batch(
+            self._h, self.device, code, tg.ctypes.data, q.ctypes.data, stride, B, C.byref(prm),
+            q_out.ctypes.data, conv.ctypes.data, iters.ctypes.data, err.ctypes.data, None,
+            _lib.IKG_FLAG_HOST_POINTERS))
+        return Solution(q_out, conv.astype(bool), iters, err)
+
+    def _solve_torch(self, targets, q0, prm, stream):
+        import torch
+        code, _ = _dtype(targets.dtype)
+        if not targets.is_cuda:
+            raise ValueError("torch targets must live on a ROCm device (or pass numpy arrays)")
+        dev = targets.device
+        tg = targets.contiguous().view(-1, 12)
+        B = tg.shape[0]
+        q = q0.to(device=dev, dtype=targets.dtype).contiguous()
+        stride = 0 if q.dim() == 1 else self.nq
+        q_out = torch.empty((B, self.nq), dtype=targets.dtype, device=dev)
+        conv = torch.empty(B, dtype=torch.uint8, device=dev)
+        iters = torch.empty(B, dtype=torch.int32, device=dev)
+        err = torch.empty((B, 2), dtype=targets.dtype, device=dev)
+        s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+        _lib.check(self.lib.ikg_solve_batch(
+            self._h, dev.index or 0, code, tg.data_ptr(), q.data_ptr(), stride, B, C.byref(prm),
+            q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(), err.data_ptr(), C.c_void_p(s), 0))
+        return Solution(q_out, conv.bool(), iters, err)
+
+    def solve_into(self, targets, q0, q_out, conv, iters, err, dtype_code, stream_handle, **kw):
+        """Raw device-pointer launch (all tensors preallocated; used by bench.py)."""
+        prm = self.params(**kw)
+        stride = 0 if q0.dim() == 1 else self.nq
+        _lib.check(self.lib.ikg_solve_batch(
+            self._h, targets.device.index or 0, dtype_code, targets.data_ptr(), q0.data_ptr(), stride,
+            targets.shape[0], C.byref(prm), q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(),
+            err.data_ptr(), C.c_void_p(stream_handle), 0))
+
+    # ------------------------------------------------------------------ multistart
+    def solve_multistart(self, targets, seeds, dtype="f64", **kw) -> Solution:
+        """S seeds x T targets -> best seed per target (ikg_solve_multistart)."""
+        prm = self.params(**kw)
+        code, npt = _dtype(dtype)
+        tg = np.ascontiguousarray(targets, dtype=npt).reshape(-1, 12)
+        sd = np.ascontiguousarray(seeds, dtype=npt).reshape(-1, self.nq)
+        T, S = tg.shape[0], sd.shape[0]
+        q_out = np.empty((T, self.nq), dtype=npt)
+        conv = np.empty(T, dtype=np.uint8)
+        iters = np.empty(T, dtype=np.int32)
+        err = np.empty((T, 2), dtype=npt)
+        best = np.empty(T, dtype=np.int32)
+        _lib.check(self.lib.ikg_solve_multistart(
+            self._h, self.device, code, tg.ctypes.data, T, sd.ctypes.data, S, C.byref(prm),
+            q_out.ctypes.data, conv.ctypes.data, iters.ctypes.data, err.ctypes.data, best.ctypes.data, None,
+            _lib.IKG_FLAG_HOST_POINTERS))
+        return Solution(q_out, conv.astype(bool), iters, err, best)
+
+    # ------------------------------------------------------------------ FK
+    def fk(self, q, dtype="f64") -> np.ndarray:
+        """Hands placements [B, 2, 12] (R row-major, t) for q [B, nq]."""
+        code, npt = _dtype(dtype)
+        qq = np.ascontiguousarray(q, dtype=npt).reshape(-1, self.nq)
+        out = np.empty((qq.shape[0], 2, 12), dtype=npt)
+        _lib.check(self.lib.ikg_fk_batch(self._h, self.device, code, qq.ctypes.data, qq.shape[0],
+                                         out.ctypes.data, None, _lib.IKG_FLAG_HOST_POINTERS))
+        return out

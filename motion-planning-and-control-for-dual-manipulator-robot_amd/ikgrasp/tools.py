@@ -1,0 +1,55 @@
+"""Mirror of the reference helpers on the IK path (tools.py).
+
+Same names and argument meaning.  `collision`/`distanceToObstacle` belong to
+the next scope row and are not provided yet: calling them
+raises NotImplementedError rather than silently answering.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .se3 import SE3, as_rt
+
+
+def jointlimitscost(robot, q):
+    """tools.py:10-13"""
+    up = max(q - robot.model.upperPositionLimit)
+    down = max(robot.model.lowerPositionLimit - q)
+    return max(0, max(up, down))
+
+
+def jointlimitsviolated(robot, q):
+    """tools.py:15-17"""
+    return jointlimitscost(robot, q) > 0.0
+
+
+def projecttojointlimits(robot, q):
+    """tools.py:21-22 — np.minimum(np.maximum(lower, q), upper)."""
+    return np.minimum(np.maximum(robot.model.lowerPositionLimit, q), robot.model.upperPositionLimit)
+
+
+def getcubeplacement(cube, hookname=None):
+    """tools.py:54-59 — oMcube (* oMf[hook] when a hook name is given).
+    Like the reference, the stored cube placement is not modified."""
+    R, t = as_rt(cube.placement)
+    oMf = SE3(R, t)
+    if hookname is not None:
+        oMf = oMf * cube.hook(hookname)
+    return oMf
+
+
+def setcubeplacement(robot, cube, oMf):
+    """tools.py:62-68 — place the cube (and the robot's copy of its collision
+    geometry) at oMf.  Callers rely on this side effect (path.py:61)."""
+    R, t = as_rt(oMf)
+    cube.placement = SE3(R, t)
+    robot.cube_placement = cube.placement
+
+
+def collision(robot, q):
+    raise NotImplementedError("collision checking is the next scope row (SURVEY §8f-1); "
+                              "computeqgrasppose reports convergence-only success")
+
+
+def distanceToObstacle(robot, q):
+    raise NotImplementedError("distance queries are out of the current scope (SURVEY §8f-2)")

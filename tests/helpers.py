@@ -1,0 +1,63 @@
+"""Vectorised numpy helpers for full-size property checks (test infrastructure).
+
+`log6_batch` restates pin.log6 over a batch; it is used to
+re-derive hand errors from FK outputs independently of the kernel's own
+reported errors.
+"""
+import numpy as np
+
+
+def log6_batch(R, p):
+    """R [N,3,3], p [N,3] -> [N,6] = [v; w]."""
+    R = np.asarray(R, dtype=np.float64)
+    p = np.asarray(p, dtype=np.float64)
+    tr = np.trace(R, axis1=1, axis2=2)
+    skew = np.stack([R[:, 2, 1] - R[:, 1, 2], R[:, 0, 2] - R[:, 2, 0], R[:, 1, 0] - R[:, 0, 1]], axis=1)
+    theta = np.arctan2(0.5 * np.linalg.norm(skew, axis=1), 0.5 * (tr - 1.0))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        f = np.where(theta > 1e-6, theta / np.sin(theta), 1.0 + theta ** 2 / 6.0) * 0.5
+    w = f[:, None] * skew
+    near_pi = theta >= np.pi - 1e-2
+    if near_pi.any():
+        i = np.nonzero(near_pi)[0]
+        cphi = np.cos(theta[i] - np.pi)
+        beta = theta[i] ** 2 / (1 + cphi)
+        tmp = (np.diagonal(R[i], axis1=1, axis2=2) + cphi[:, None]) * beta[:, None]
+        sg = np.where(skew[i] > 0, 1.0, -1.0)
+        w[i] = sg * np.sqrt(np.maximum(tmp, 0.0))
+    t2 = theta ** 2
+    with np.errstate(divide="ignore", invalid="ignore"):
+        small = theta < 1e-3
+        st, ct = np.sin(theta), np.cos(theta)
+        alpha = np.where(small, 1 - t2 / 12 - t2 * t2 / 720, theta * st / (2 * (1 - ct)))
+        beta = np.where(small, 1.0 / 12 + t2 / 720, 1 / t2 - st / (2 * theta * (1 - ct)))
+    wp = np.sum(w * p, axis=1)
+    v = alpha[:, None] * p - 0.5 * np.cross(w, p) + (beta * wp)[:, None] * w
+    return np.concatenate([v, w], axis=1)
+
+
+def se3_err(Ra, ta, Rb, tb):
+    """|log6(Ma^-1 Mb)| for batches."""
+    Rm = np.einsum("nji,njk->nik", Ra, Rb)
+    pm = np.einsum("nji,nj->ni", Ra, tb - ta)
+    return np.linalg.norm(log6_batch(Rm, pm), axis=1)
+
+
+def hook_targets(model, targets):
+    """[B,12] cube placements -> per-hand target (R [B,2,3,3], t [B,2,3])."""
+    CR = targets[:, :9].reshape(-1, 3, 3)
+    Ct = targets[:, 9:]
+    R = np.einsum("bij,hjk->bhik", CR, model.hook_R)
+    t = Ct[:, None, :] + np.einsum("bij,hj->bhi", CR, model.hook_t)
+    return R, t
+
+
+def hand_errors_from_fk(model, hands, targets):
+    """hands [B,2,12] (from ikg_fk_batch) + cube targets -> [B,2] |log6| errors."""
+    TR, Tt = hook_targets(model, np.asarray(targets, dtype=np.float64))
+    out = np.empty((hands.shape[0], 2))
+    for h in range(2):
+        Rh = hands[:, h, :9].reshape(-1, 3, 3).astype(np.float64)
+        th = hands[:, h, 9:].astype(np.float64)
+        out[:, h] = se3_err(Rh, th, TR[:, h], Tt[:, h])
+    return out

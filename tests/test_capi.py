@@ -1,0 +1,91 @@
+"""C-ABI surface on CPU: the library loads, exports every symbol the header
+declares, validates models/arguments and reports errors through
+ikg_last_error — no compute calls (there is no GPU here)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from ikgrasp import _lib
+from ikgrasp.model import load_nextage
+
+HEADER = os.path.join(os.path.dirname(__file__), "..", "include", "ikgrasp.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?(?:int|void|char\s*\*|const char\s*\*)\s*\*?\s*(ikg_\w+)\s*\(",
+                                 text, re.M)))
+
+
+def test_header_declares_expected_api():
+    assert declared_symbols() == sorted(_lib.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.load()
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_defaults_match_reference():
+    p = _lib.default_params()
+    assert p.eps == 1e-3 and p.dt == 1e-2 and p.max_iters == 1000 and p.lambda_ == 0.0
+    assert _lib.load().ikg_version().startswith(b"ikgrasp")
+
+
+def test_model_create_destroy():
+    lib = _lib.load()
+    d = _lib.model_desc(load_nextage())
+    h = C.c_void_p()
+    assert lib.ikg_model_create(C.byref(d), C.byref(h)) == 0 and h.value
+    lib.ikg_model_destroy(h)
+
+
+@pytest.mark.parametrize("mutate,msg", [
+    (lambda d: setattr(d, "nq", 0), "nq"),
+    (lambda d: d.axis.__setitem__(4, 7), "axis"),
+    (lambda d: d.arm_q[0].__setitem__(2, 9), "arm"),
+    (lambda d: d.parent.__setitem__(5, 9), "parent"),
+    (lambda d: d.axis.__setitem__(12, 2), "axes differ"),
+])
+def test_model_create_rejects_bad_structure(mutate, msg):
+    lib = _lib.load()
+    d = _lib.model_desc(load_nextage())
+    mutate(d)
+    h = C.c_void_p()
+    rc = lib.ikg_model_create(C.byref(d), C.byref(h))
+    assert rc == -1
+    assert msg in lib.ikg_last_error().decode()
+
+
+def test_solve_rejects_bad_arguments_before_touching_the_device():
+    lib = _lib.load()
+    d = _lib.model_desc(load_nextage())
+    h = C.c_void_p()
+    assert lib.ikg_model_create(C.byref(d), C.byref(h)) == 0
+    p = _lib.default_params()
+    p.eps = -1.0
+    rc = lib.ikg_solve_batch(h, 0, 0, None, None, 0, 4, C.byref(p), None, None, None, None, None, 0)
+    assert rc == -1 and "required" in lib.ikg_last_error().decode()
+    buf = (C.c_double * 64)()
+    rc = lib.ikg_solve_batch(h, 0, 0, buf, buf, 0, 1, C.byref(p), buf, None, None, None, None, 0)
+    assert rc == -1 and "eps" in lib.ikg_last_error().decode()
+    p = _lib.default_params()
+    rc = lib.ikg_solve_batch(h, 0, 5, buf, buf, 0, 1, C.byref(p), buf, None, None, None, None, 0)
+    assert rc == -1 and "dtype" in lib.ikg_last_error().decode()
+    rc = lib.ikg_solve_multistart(h, 0, 0, buf, 1, buf, 1000, C.byref(p), buf, None, None, None, None, None, 0)
+    assert rc == -1 and "seeds" in lib.ikg_last_error().decode()
+    lib.ikg_model_destroy(h)
+
+
+def test_no_device_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from ikgrasp.solver import IKSolver
+    import numpy as np
+    s = IKSolver()
+    with pytest.raises(_lib.IkgError):
+        s.solve(np.zeros((1, 12)), np.zeros(15))

@@ -1,0 +1,33 @@
+"""Compile the reference scene's URDFs into the kernel's model tables.
+
+    python tools/compile_model.py [/root/reference]
+
+Writes `<pkg>/ikgrasp/data/nextage_dualarm.json` (committed: the GPU box has
+no reference tree).  Inputs: `models/nextagea_description/urdf/NextageaOpen.urdf`
+and `models/cubes/cube_small.urdf` (config.py:44-51), base placement
+ROBOT_PLACEMENT = (I, [0, 0, 0.85]) (config.py:33).
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "motion-planning-and-control-for-dual-manipulator-robot_amd"))
+
+from ikgrasp.model import DualArmModel, NEXTAGE_JSON  # noqa: E402
+
+
+def main(ref="/root/reference"):
+    robot = os.path.join(ref, "models/nextagea_description/urdf/NextageaOpen.urdf")
+    cube = os.path.join(ref, "models/cubes/cube_small.urdf")
+    base = (np.eye(3), np.array([0.0, 0.0, 0.85]))
+    m = DualArmModel.from_urdf(robot, cube, base_placement=base)
+    os.makedirs(os.path.dirname(NEXTAGE_JSON), exist_ok=True)
+    with open(NEXTAGE_JSON, "w") as f:
+        f.write(m.to_json())
+    print(f"wrote {NEXTAGE_JSON}: nq={m.nq} root={m.root_q} arms={m.arm_q.tolist()}")
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
