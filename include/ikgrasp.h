@@ -131,6 +131,12 @@ int ikg_solve_multistart(const ikg_model* model, int device, int dtype,
 int ikg_fk_batch(const ikg_model* model, int device, int dtype,
                  const void* q, int64_t B, void* hands, void* stream, uint32_t flags);
 
+/*
+ * Batched SE(3) logarithm, pin.log6 (the pose error of
+ * inverse_geometry.py:66-67): M [B,12] -> out [B,6] = [v; w].
+ */
+int ikg_log6_batch(int device, int dtype, const void* M, int64_t B, void* out, void* stream, uint32_t flags);
+
 /* Thread-local message of the last failure ("" if none). */
 const char* ikg_last_error(void);
 

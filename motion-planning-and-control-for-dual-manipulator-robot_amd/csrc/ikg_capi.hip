@@ -15,6 +15,7 @@
 
 #include "ikg_device.hpp"
 #include "ikg_launch.hpp"
+#include "ikg_model_build.hpp"
 #include "ikgrasp.h"
 
 namespace {
@@ -31,55 +32,6 @@ int fail(int code, const char* fmt, ...) {
 
 int hip_fail(hipError_t e, const char* what) {
   return fail(IKG_EHIP, "%s: %s", what, hipGetErrorString(e));
-}
-
-bool is_identity(const double* R) {
-  for (int r = 0; r < 3; ++r)
-    for (int c = 0; c < 3; ++c)
-      if (R[3 * r + c] != (r == c ? 1.0 : 0.0)) return false;
-  return true;
-}
-
-template <typename T>
-void build_kmodel(const ikg_model_desc& d, ikg::KModel<T>& k) {
-  std::memset(&k, 0, sizeof(k));
-  const int r = d.root_q;
-  for (int i = 0; i < 9; ++i) k.root_R[i] = (T)d.placement[r][i];
-  for (int i = 0; i < 3; ++i) k.root_t[i] = (T)d.placement[r][9 + i];
-  k.root_lo = (T)d.lower[r];
-  k.root_hi = (T)d.upper[r];
-  k.root_q = r;
-  k.root_axis = d.axis[r];
-  k.rot_mask = 0;
-  for (int a = 0; a < 2; ++a)
-    for (int j = 0; j < IKG_ARM_DOF; ++j) {
-      const int q = d.arm_q[a][j];
-      for (int i = 0; i < 9; ++i) k.arm_R[a][j][i] = (T)d.placement[q][i];
-      for (int i = 0; i < 3; ++i) k.arm_t[a][j][i] = (T)d.placement[q][9 + i];
-      k.arm_lo[a][j] = (T)d.lower[q];
-      k.arm_hi[a][j] = (T)d.upper[q];
-      k.arm_q[a][j] = q;
-      k.arm_axis[j] = d.axis[q];
-      if (!is_identity(d.placement[q])) k.rot_mask |= 1 << j;
-    }
-  for (int a = 0; a < 2; ++a) {
-    for (int i = 0; i < 9; ++i) k.hand_R[a][i] = (T)d.hand[a][i];
-    for (int i = 0; i < 3; ++i) k.hand_t[a][i] = (T)d.hand[a][9 + i];
-    for (int i = 0; i < 9; ++i) k.hook_R[a][i] = (T)d.hook[a][i];
-    for (int i = 0; i < 3; ++i) k.hook_t[a][i] = (T)d.hook[a][9 + i];
-  }
-  for (int q = 0; q < d.nq; ++q) {
-    k.lo[q] = (T)d.lower[q];
-    k.hi[q] = (T)d.upper[q];
-  }
-  k.nq = d.nq;
-  bool used[IKG_MAX_NQ] = {};
-  used[r] = true;
-  for (int a = 0; a < 2; ++a)
-    for (int j = 0; j < IKG_ARM_DOF; ++j) used[d.arm_q[a][j]] = true;
-  k.n_passive = 0;
-  for (int q = 0; q < d.nq; ++q)
-    if (!used[q]) k.passive_q[k.n_passive++] = q;
 }
 
 }  // namespace
@@ -302,9 +254,74 @@ int fk_t(ikg_model* model, int device, const void* q, int64_t B, void* hands, hi
   return IKG_OK;
 }
 
+template <typename T>
+int log6_t(const void* M, int64_t B, void* out, hipStream_t s, uint32_t flags) {
+  Staging st(s);
+  const bool host = flags & IKG_FLAG_HOST_POINTERS;
+  const void* dm = M;
+  void* dout = out;
+  if (host) {
+    dm = st.in(M, sizeof(T) * 12 * B);
+    dout = st.out(sizeof(T) * 6 * B);
+    if (st.rc) return st.rc;
+  }
+  hipError_t e = ikg::launch_log6<T>(dm, B, dout, s);
+  if (e != hipSuccess) return hip_fail(e, "ikg log6 kernel launch");
+  if (host) {
+    st.back(out, dout, sizeof(T) * 6 * B);
+    if (st.rc) return st.rc;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
+  return IKG_OK;
+}
+
+template <typename T>
+int pair_state_t(ikg_model* model, int device, const void* targets, const void* q0, int64_t B, void* out) {
+  const ikg::KModel<T>* dm = nullptr;
+  int rc = model->device_tables<T>(device, &dm);
+  if (rc) return rc;
+  Staging st(0);
+  const void* dt = st.in(targets, sizeof(T) * 12 * B);
+  const void* dq = st.in(q0, sizeof(T) * model->desc.nq);
+  void* dout = st.out(sizeof(T) * 62 * B);
+  if (st.rc) return st.rc;
+  hipError_t e = ikg::launch_pair_state<T>(dm, dt, dq, 0, B, dout, 0);
+  if (e != hipSuccess) return hip_fail(e, "pair state kernel");
+  st.back(out, dout, sizeof(T) * 62 * B);
+  if (st.rc) return st.rc;
+  e = hipStreamSynchronize(0);
+  return e == hipSuccess ? IKG_OK : hip_fail(e, "hipStreamSynchronize");
+}
+
 }  // namespace
 
 extern "C" {
+
+// Diagnostic (not in include/ikgrasp.h): per-lane iteration-0 state of the
+// pair kernel, host pointers, q0 broadcast; out [B,2,31].
+int ikg_debug_pair_state(const ikg_model* model, int device, int dtype, const void* targets, const void* q0,
+                         int64_t B, void* out) {
+  g_err[0] = 0;
+  if (!model || B < 0) return fail(IKG_EINVAL, "bad arguments");
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  return dtype == IKG_F64 ? pair_state_t<double>(m, device, targets, q0, B, out)
+                          : pair_state_t<float>(m, device, targets, q0, B, out);
+}
+
+int ikg_log6_batch(int device, int dtype, const void* M, int64_t B, void* out, void* stream, uint32_t flags) {
+  g_err[0] = 0;
+  if (B < 0) return fail(IKG_EINVAL, "B must be >= 0");
+  if (B > 0 && (!M || !out)) return fail(IKG_EINVAL, "M and out are required");
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  if (B == 0) return IKG_OK;
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == IKG_F64 ? log6_t<double>(M, B, out, s, flags) : log6_t<float>(M, B, out, s, flags);
+}
 
 const char* ikg_last_error(void) { return g_err; }
 
@@ -347,14 +364,11 @@ int ikg_model_create(const ikg_model_desc* d, ikg_model** out) {
   for (int j = 0; j < IKG_ARM_DOF; ++j)
     if (d->axis[d->arm_q[0][j]] != d->axis[d->arm_q[1][j]])
       return fail(IKG_EINVAL, "arm joint %d: left/right axes differ (unsupported)", j);
-  if (!is_identity(d->placement[r])) {
-    // the root rotation is applied through rotate_axis(root_R): any rotation works
-  }
-  ikg_model* m = new (std::nothrow) ikg_model();
+    ikg_model* m = new (std::nothrow) ikg_model();
   if (!m) return fail(IKG_ENOMEM, "out of host memory");
   m->desc = *d;
-  build_kmodel<double>(*d, m->k64);
-  build_kmodel<float>(*d, m->k32);
+  ikg::build_kmodel<double>(*d, m->k64);
+  ikg::build_kmodel<float>(*d, m->k32);
   *out = m;
   return IKG_OK;
 }

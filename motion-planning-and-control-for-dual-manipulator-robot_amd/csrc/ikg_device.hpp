@@ -9,6 +9,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// Math helpers are __host__ __device__ so tools/host_emu.cpp can run the
+// exact kernel arithmetic on the CPU for debugging (never a product path).
+#define IKG_HD __host__ __device__
+
 namespace ikg {
 
 constexpr int kArmDof = 6;
@@ -60,7 +64,7 @@ struct Prec<double> {
   static constexpr double kPi = 3.14159265358979323846;
   // relative cut-off for the triangular solve (np.linalg.pinv rcond = 1e-15)
   static constexpr double kRcond = 1e-15;
-  __device__ static inline void sincos_(double x, double* s, double* c) { ::sincos(x, s, c); }
+  IKG_HD static inline void sincos_(double x, double* s, double* c) { ::sincos(x, s, c); }
 };
 
 template <>
@@ -71,11 +75,11 @@ struct Prec<float> {
   static constexpr float kPrec3 = 0.1f;
   static constexpr float kPi = 3.14159265358979323846f;
   static constexpr float kRcond = 1e-7f;
-  __device__ static inline void sincos_(float x, float* s, float* c) { ::sincosf(x, s, c); }
+  IKG_HD static inline void sincos_(float x, float* s, float* c) { ::sincosf(x, s, c); }
 };
 
 template <typename T>
-__device__ inline T sel(bool b, T x, T y) { return b ? x : y; }
+IKG_HD inline T sel(bool b, T x, T y) { return b ? x : y; }
 
 // ---------------------------------------------------------------- cross-lane
 // Exchange a value with the partner lane (lane ^ 1) through a DPP quad_perm
@@ -96,7 +100,7 @@ __device__ inline double pair_swap(double x) {
 // ---------------------------------------------------------------- SE(3) pieces
 // R is row-major: R[3*r + c].
 template <typename T>
-__device__ inline void matmul3(const T* A, const T* B, T* C) {
+IKG_HD inline void matmul3(const T* A, const T* B, T* C) {
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -106,7 +110,7 @@ __device__ inline void matmul3(const T* A, const T* B, T* C) {
 
 // C = A^T B
 template <typename T>
-__device__ inline void matmul3_tn(const T* A, const T* B, T* C) {
+IKG_HD inline void matmul3_tn(const T* A, const T* B, T* C) {
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -115,13 +119,13 @@ __device__ inline void matmul3_tn(const T* A, const T* B, T* C) {
 }
 
 template <typename T>
-__device__ inline void matvec3(const T* A, const T* x, T* y) {
+IKG_HD inline void matvec3(const T* A, const T* x, T* y) {
 #pragma unroll
   for (int r = 0; r < 3; ++r) y[r] = A[3 * r] * x[0] + A[3 * r + 1] * x[1] + A[3 * r + 2] * x[2];
 }
 
 template <typename T>
-__device__ inline void matvec3_t(const T* A, const T* x, T* y) {
+IKG_HD inline void matvec3_t(const T* A, const T* x, T* y) {
 #pragma unroll
   for (int r = 0; r < 3; ++r) y[r] = A[r] * x[0] + A[3 + r] * x[1] + A[6 + r] * x[2];
 }
@@ -129,7 +133,7 @@ __device__ inline void matvec3_t(const T* A, const T* x, T* y) {
 // R <- R * Rot_axis(q) given (s, c) = sincos(q): JointModelR{X,Y,Z}::calc
 // composed onto the parent rotation (only two columns change).
 template <typename T>
-__device__ inline void rotate_axis(T* R, int axis, T s, T c) {
+IKG_HD inline void rotate_axis(T* R, int axis, T s, T c) {
   if (axis == 0) {
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -155,7 +159,7 @@ __device__ inline void rotate_axis(T* R, int axis, T s, T c) {
 }
 
 template <typename T>
-__device__ inline void column(const T* R, int axis, T* a) {
+IKG_HD inline void column(const T* R, int axis, T* a) {
   a[0] = axis == 0 ? R[0] : (axis == 1 ? R[1] : R[2]);
   a[1] = axis == 0 ? R[3] : (axis == 1 ? R[4] : R[5]);
   a[2] = axis == 0 ? R[6] : (axis == 1 ? R[7] : R[8]);
@@ -165,7 +169,7 @@ __device__ inline void column(const T* R, int axis, T* a) {
 // pin.log3 (2.6-era branch structure) and pin.log6 ->
 // [v; w] (inverse_geometry.py:66-67).
 template <typename T>
-__device__ inline void log6(const T* R, const T* p, T* e) {
+IKG_HD inline void log6(const T* R, const T* p, T* e) {
   const T pi = Prec<T>::kPi;
   const T tr = R[0] + R[4] + R[8];
   const T sx = R[7] - R[5], sy = R[2] - R[6], sz = R[3] - R[1];
@@ -242,7 +246,7 @@ __device__ inline void log6(const T* R, const T* p, T* e) {
 //   Rh, th  : effector frame placement oMf (data.oMf[LARM/RARM_EFF], :62-63)
 //   ax, org : world axis / origin of the 7 supporting joints (root first)
 template <typename T, bool WANT_AXES>
-__device__ inline void fk_arm(const KModel<T>* __restrict__ m, int arm, T qc, const T* qa, T* Rh, T* th,
+IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, T qc, const T* qa, T* Rh, T* th,
                               T (*ax)[3], T (*org)[3]) {
   T R[9], t[3];
   T s, c;
@@ -297,7 +301,7 @@ __device__ inline void fk_arm(const KModel<T>* __restrict__ m, int arm, T qc, co
 
 // log6(oMhand^-1 * oMtarget) (inverse_geometry.py:66-67)
 template <typename T>
-__device__ inline void pose_error(const T* Rh, const T* th, const T* RT, const T* tT, T* e) {
+IKG_HD inline void pose_error(const T* Rh, const T* th, const T* RT, const T* tT, T* e) {
   T Rm[9], d[3], pm[3];
   matmul3_tn(Rh, RT, Rm);
 #pragma unroll
@@ -312,7 +316,7 @@ __device__ inline void pose_error(const T* Rh, const T* th, const T* RT, const T
 // x = A^-1 b for both.  Diagonal entries below rcond * max|R_kk| are
 // truncated to a zero inverse (the analogue of pinv's rcond).
 template <typename T>
-__device__ inline void qr_solve6(T (&A)[6][8], T* x0, T* x1) {
+IKG_HD inline void qr_solve6(T (&A)[6][8], T* x0, T* x1) {
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     T n2 = T(0);
@@ -358,7 +362,7 @@ __device__ inline void qr_solve6(T (&A)[6][8], T* x0, T* x1) {
 
 // Cholesky solve of the damped arm block (J_a J_a^T + lambda I) for 2 RHS.
 template <typename T>
-__device__ inline void chol_solve6(T (&M)[6][6], T* b0, T* b1) {
+IKG_HD inline void chol_solve6(T (&M)[6][6], T* b0, T* b1) {
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
     T d = M[k][k];
@@ -397,9 +401,138 @@ __device__ inline void chol_solve6(T (&M)[6][6], T* b0, T* b1) {
 }
 
 template <typename T>
-__device__ inline T clampq(T q, T lo, T hi) {
+IKG_HD inline T clampq(T q, T lo, T hi) {
   // np.minimum(np.maximum(lower, q), upper)  (tools.py:21-22)
   return fmin(fmax(lo, q), hi);
 }
+
+// ---------------------------------------------------------------- per-lane iteration stages
+// One arm-lane's share of an iteration of inverse_geometry.py:56-89.  The
+// kernel composes these with DPP exchanges (ikg_kernels.hip solve_pair);
+// tools/host_emu.cpp composes the same functions for both arms on the CPU.
+template <typename T>
+struct ArmState {
+  T Rh[9], th[3];       // effector placement oMf
+  T ax[7][3], org[7][3];  // world axis / origin of root + arm joints
+  T e[6];               // log6(oMf^-1 oMtarget)
+};
+
+// FK + pose error; returns |e| (inverse_geometry.py:58-67).
+template <typename T>
+IKG_HD inline T arm_fk_error(const KModel<T>* __restrict__ m, int arm, T qc, const T* qa, const T* RT, const T* tT,
+                             ArmState<T>& st) {
+  fk_arm<T, true>(m, arm, qc, qa, st.Rh, st.th, st.ax, st.org);
+  pose_error(st.Rh, st.th, RT, tT, st.e);
+  const T* e = st.e;
+  return sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3] + e[4] * e[4] + e[5] * e[5]);
+}
+
+// World-aligned Jacobian at the hand point, col_j = [a_j x (p_h - o_j); a_j]
+// (columns 0..5 = arm joints, 7 = root) and the rotated error Rh e (column 6).
+// LOCAL = blockdiag(Rh^T, Rh^T) * world-aligned (:75-76), and the rotation is
+// orthogonal, so the minimum-norm step is unchanged.
+template <typename T>
+IKG_HD inline void arm_system(const ArmState<T>& st, T (&A)[6][8]) {
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int col = j == 0 ? 7 : j - 1;
+    const T dx = st.th[0] - st.org[j][0], dy = st.th[1] - st.org[j][1], dz = st.th[2] - st.org[j][2];
+    A[0][col] = st.ax[j][1] * dz - st.ax[j][2] * dy;
+    A[1][col] = st.ax[j][2] * dx - st.ax[j][0] * dz;
+    A[2][col] = st.ax[j][0] * dy - st.ax[j][1] * dx;
+    A[3][col] = st.ax[j][0];
+    A[4][col] = st.ax[j][1];
+    A[5][col] = st.ax[j][2];
+  }
+  T ev[3], ew[3];
+  matvec3(st.Rh, st.e, ev);
+  matvec3(st.Rh, st.e + 3, ew);
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    A[r][6] = ev[r];
+    A[3 + r][6] = ew[r];
+  }
+}
+
+// lambda = 0: u = J_a^-1 e_a, v = J_a^-1 c_a; alpha = u.v, beta = v.v.
+template <typename T>
+IKG_HD inline void arm_solve(T (&A)[6][8], T* u, T* v, T& alpha, T& beta) {
+  qr_solve6(A, u, v);
+  alpha = T(0);
+  beta = T(0);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    alpha += u[k] * v[k];
+    beta += v[k] * v[k];
+  }
+}
+
+// lambda > 0: z_e, z_c = (J_a J_a^T + lambda I)^-1 [e_a, c_a]; alpha = c.z_e, beta = c.z_c.
+template <typename T>
+IKG_HD inline void arm_solve_damped(const T (&A)[6][8], T lambda, T* ze, T* zc, T& alpha, T& beta) {
+  T M[6][6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = 0; c <= r; ++c) {
+      T acc = r == c ? lambda : T(0);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) acc += A[r][k] * A[c][k];
+      M[r][c] = acc;
+    }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    ze[r] = A[r][6];
+    zc[r] = A[r][7];
+  }
+  chol_solve6(M, ze, zc);
+  alpha = T(0);
+  beta = T(0);
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    alpha += A[r][7] * ze[r];
+    beta += A[r][7] * zc[r];
+  }
+}
+
+// Sherman–Morrison chest step from the pair-summed scalars.
+template <typename T>
+IKG_HD inline T chest_step(T alpha_sum, T beta_sum) {
+  return alpha_sum / (T(1) + beta_sum);
+}
+
+template <typename T>
+IKG_HD inline void arm_dq(const T* u, const T* v, T s, T* dq) {
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dq[k] = u[k] - s * v[k];
+}
+
+template <typename T>
+IKG_HD inline void arm_dq_damped(const T (&A)[6][8], const T* ze, const T* zc, T s, T* dq) {
+  T y[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) y[r] = ze[r] - s * zc[r];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    T acc = T(0);
+#pragma unroll
+    for (int r = 0; r < 6; ++r) acc += A[r][k] * y[r];
+    dq[k] = acc;
+  }
+}
+
+// pin.integrate (q + dq * DT, :86) then projecttojointlimits (:89).
+template <typename T>
+IKG_HD inline void arm_update(const KModel<T>* __restrict__ m, int arm, T dt, T s, const T* dq, T& qc, T* qa) {
+  const bool right = arm != 0;
+  qc = clampq(qc + s * dt, m->root_lo, m->root_hi);
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) {
+    const T lo = sel(right, m->arm_lo[1][k], m->arm_lo[0][k]);
+    const T hi = sel(right, m->arm_hi[1][k], m->arm_hi[0][k]);
+    qa[k] = clampq(qa[k] + dq[k] * dt, lo, hi);
+  }
+}
+
 
 }  // namespace ikg

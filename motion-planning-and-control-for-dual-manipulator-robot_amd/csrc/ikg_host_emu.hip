@@ -1,0 +1,100 @@
+// Host emulator of the pair kernel (debug/test tool, NOT a product path and
+// never called by libikgrasp.so): runs the exact stage functions of
+// ikg_device.hpp for both arm lanes of a problem on the CPU, in the order the
+// kernel's lanes execute them, so kernel numerics can be inspected without a
+// GPU.  Built as libikgrasp_emu.so; used by tests/test_host_emu.py.
+#include <cstdint>
+#include <cstring>
+
+#include "ikg_device.hpp"
+#include "ikg_model_build.hpp"
+#include "ikgrasp.h"
+
+namespace {
+
+template <typename T>
+void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, const T* tg, const T* qrow,
+             T* qo, uint8_t* conv_out, int32_t* iters_out, T* err_out, T* trace, int trace_len) {
+  using namespace ikg;
+  T RT[2][9], tT[2][3], qc[2], qa[2][kArmDof];
+  for (int arm = 0; arm < 2; ++arm) {
+    const bool right = arm != 0;
+    T HR[9], Ht[3], d[3];
+    for (int i = 0; i < 9; ++i) HR[i] = right ? m.hook_R[1][i] : m.hook_R[0][i];
+    for (int i = 0; i < 3; ++i) Ht[i] = right ? m.hook_t[1][i] : m.hook_t[0][i];
+    matmul3(tg, HR, RT[arm]);
+    matvec3(tg, Ht, d);
+    for (int i = 0; i < 3; ++i) tT[arm][i] = tg[9 + i] + d[i];
+    qc[arm] = qrow[m.root_q];
+    for (int k = 0; k < kArmDof; ++k) qa[arm][k] = qrow[m.arm_q[arm][k]];
+  }
+  int it = 0;
+  bool conv = false;
+  T nrm[2];
+  for (;;) {
+    ArmState<T> st[2];
+    for (int arm = 0; arm < 2; ++arm) nrm[arm] = arm_fk_error(&m, arm, qc[arm], qa[arm], RT[arm], tT[arm], st[arm]);
+    if (trace && it < trace_len) {
+      trace[2 * it] = nrm[0];
+      trace[2 * it + 1] = nrm[1];
+    }
+    if (it >= prm.max_iters) break;
+    if (nrm[0] < prm.eps && nrm[1] < prm.eps) {
+      conv = true;
+      break;
+    }
+    T A[2][6][8], u[2][6], v[2][6], al[2], be[2], dq[6];
+    for (int arm = 0; arm < 2; ++arm) {
+      arm_system(st[arm], A[arm]);
+      if (damped)
+        arm_solve_damped(A[arm], prm.lambda, u[arm], v[arm], al[arm], be[arm]);
+      else
+        arm_solve(A[arm], u[arm], v[arm], al[arm], be[arm]);
+    }
+    for (int arm = 0; arm < 2; ++arm) {
+      const T s = chest_step(al[arm] + al[1 - arm], be[arm] + be[1 - arm]);
+      if (damped)
+        arm_dq_damped(A[arm], u[arm], v[arm], s, dq);
+      else
+        arm_dq(u[arm], v[arm], s, dq);
+      arm_update(&m, arm, prm.dt, s, dq, qc[arm], qa[arm]);
+    }
+    ++it;
+  }
+  for (int j = 0; j < m.nq; ++j) qo[j] = qrow[j];
+  for (int i = 0; i < m.n_passive; ++i) {
+    const int j = m.passive_q[i];
+    qo[j] = it > 0 ? clampq(qrow[j], m.lo[j], m.hi[j]) : qrow[j];
+  }
+  qo[m.root_q] = qc[0];
+  for (int arm = 0; arm < 2; ++arm)
+    for (int k = 0; k < kArmDof; ++k) qo[m.arm_q[arm][k]] = qa[arm][k];
+  *conv_out = conv;
+  *iters_out = it;
+  err_out[0] = nrm[0];
+  err_out[1] = nrm[1];
+}
+
+template <typename T>
+void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t stride, int64_t B,
+         const ikg_params* p, void* q_out, uint8_t* conv, int32_t* iters, void* err, void* trace, int trace_len) {
+  ikg::KModel<T> m;
+  ikg::build_kmodel<T>(*d, m);
+  ikg::KParams<T> prm{(T)p->eps, (T)p->dt, (T)p->lambda, p->max_iters};
+  for (int64_t i = 0; i < B; ++i)
+    emu_one<T>(m, prm, p->lambda > 0, (const T*)targets + 12 * i, (const T*)q0 + stride * i,
+               (T*)q_out + d->nq * i, conv + i, iters + i, (T*)err + 2 * i,
+               trace ? (T*)trace + (int64_t)2 * trace_len * i : nullptr, trace_len);
+}
+
+}  // namespace
+
+extern "C" int ikg_emu_solve(const ikg_model_desc* d, int dtype, const void* targets, const void* q0,
+                             int64_t q0_stride, int64_t B, const ikg_params* p, void* q_out, uint8_t* conv,
+                             int32_t* iters, void* err, void* trace, int trace_len) {
+  if (dtype == IKG_F64)
+    emu<double>(d, targets, q0, q0_stride, B, p, q_out, conv, iters, err, trace, trace_len);
+  else
+    emu<float>(d, targets, q0, q0_stride, B, p, q_out, conv, iters, err, trace, trace_len);
+  return 0;
+}

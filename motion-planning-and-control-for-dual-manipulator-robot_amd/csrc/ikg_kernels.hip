@@ -31,109 +31,33 @@ template <typename T, bool DAMPED>
 __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, const T* RT,
                                   const T* tT, T& qc, T* qa, int& it_out, bool& conv_out, T& nrm_out,
                                   T& other_out) {
-  const bool right = arm != 0;
-  const T root_lo = m->root_lo, root_hi = m->root_hi;
   int it = 0;
   bool conv = false;
   T nrm, other;
   for (;;) {
-    T Rh[9], th[3], ax[7][3], org[7][3];
-    fk_arm<T, true>(m, arm, qc, qa, Rh, th, ax, org);
-    T e[6];
-    pose_error(Rh, th, RT, tT, e);
-    nrm = sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3] + e[4] * e[4] + e[5] * e[5]);
+    ArmState<T> st;
+    nrm = arm_fk_error(m, arm, qc, qa, RT, tT, st);
     other = pair_swap(nrm);
     if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
     if (nrm < prm.eps && other < prm.eps) {
       conv = true;
       break;
     }
-    // World-aligned Jacobian at the hand point: col_j = [a_j x (p_h - o_j); a_j].
-    // LOCAL = blockdiag(Rh^T, Rh^T) * world-aligned, so solving with the
-    // rotated error Rh e gives the same dq (the rotation is orthogonal).
     T A[6][8];
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const int col = j == 0 ? 7 : j - 1;
-      const T dx = th[0] - org[j][0], dy = th[1] - org[j][1], dz = th[2] - org[j][2];
-      A[0][col] = ax[j][1] * dz - ax[j][2] * dy;
-      A[1][col] = ax[j][2] * dx - ax[j][0] * dz;
-      A[2][col] = ax[j][0] * dy - ax[j][1] * dx;
-      A[3][col] = ax[j][0];
-      A[4][col] = ax[j][1];
-      A[5][col] = ax[j][2];
-    }
-    T ev[3], ew[3];
-    matvec3(Rh, e, ev);
-    matvec3(Rh, e + 3, ew);
-    A[0][6] = ev[0];
-    A[1][6] = ev[1];
-    A[2][6] = ev[2];
-    A[3][6] = ew[0];
-    A[4][6] = ew[1];
-    A[5][6] = ew[2];
-
-    T dq[6], s;
+    arm_system(st, A);
+    T dq[6], alpha, beta;
     if constexpr (!DAMPED) {
       T u[6], v[6];
-      qr_solve6(A, u, v);
-      T alpha = T(0), beta = T(0);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        alpha += u[k] * v[k];
-        beta += v[k] * v[k];
-      }
-      const T at = alpha + pair_swap(alpha);
-      const T bt = beta + pair_swap(beta);
-      s = at / (T(1) + bt);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) dq[k] = u[k] - s * v[k];
+      arm_solve(A, u, v, alpha, beta);
+      const T s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+      arm_dq(u, v, s, dq);
+      arm_update(m, arm, prm.dt, s, dq, qc, qa);
     } else {
-      // (J J^T + lambda I) y = e with J J^T = blockdiag(J_L J_L^T, J_R J_R^T) + c c^T
-      T M[6][6];
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = 0; c <= r; ++c) {
-          T acc = r == c ? prm.lambda : T(0);
-#pragma unroll
-          for (int k = 0; k < 6; ++k) acc += A[r][k] * A[c][k];
-          M[r][c] = acc;
-        }
       T ze[6], zc[6];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        ze[r] = A[r][6];
-        zc[r] = A[r][7];
-      }
-      chol_solve6(M, ze, zc);
-      T alpha = T(0), beta = T(0);
-#pragma unroll
-      for (int r = 0; r < 6; ++r) {
-        alpha += A[r][7] * ze[r];
-        beta += A[r][7] * zc[r];
-      }
-      const T at = alpha + pair_swap(alpha);
-      const T bt = beta + pair_swap(beta);
-      s = at / (T(1) + bt);
-      T y[6];
-#pragma unroll
-      for (int r = 0; r < 6; ++r) y[r] = ze[r] - s * zc[r];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) {
-        T acc = T(0);
-#pragma unroll
-        for (int r = 0; r < 6; ++r) acc += A[r][k] * y[r];
-        dq[k] = acc;
-      }
-    }
-    // pin.integrate (q + dq * DT) then projecttojointlimits
-    qc = clampq(qc + s * prm.dt, root_lo, root_hi);
-#pragma unroll
-    for (int k = 0; k < kArmDof; ++k) {
-      const T lo = sel(right, m->arm_lo[1][k], m->arm_lo[0][k]);
-      const T hi = sel(right, m->arm_hi[1][k], m->arm_hi[0][k]);
-      qa[k] = clampq(qa[k] + dq[k] * prm.dt, lo, hi);
+      arm_solve_damped(A, prm.lambda, ze, zc, alpha, beta);
+      const T s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+      arm_dq_damped(A, ze, zc, s, dq);
+      arm_update(m, arm, prm.dt, s, dq, qc, qa);
     }
     ++it;
   }
@@ -301,6 +225,47 @@ __global__ __launch_bounds__(256) void ikg_fk_kernel(const KModel<T>* __restrict
   }
 }
 
+// Diagnostic: each lane of the pair layout dumps its iteration-0 state
+// [RT(9) tT(3) Rh(9) th(3) e(6) |e|] = 31 values (tests/test_gpu_parity.py).
+template <typename T>
+__global__ __launch_bounds__(64) void ikg_pair_state_kernel(const KModel<T>* __restrict__ m,
+                                                            const T* __restrict__ targets,
+                                                            const T* __restrict__ q0, int64_t q0_stride, int64_t B,
+                                                            T* __restrict__ out) {
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t p = gid >> 1;
+  const int arm = (int)(gid & 1);
+  if (p >= B) return;
+  T RT[9], tT[3];
+  hook_target(m, arm, targets + p * 12, RT, tT);
+  T qc, qa[kArmDof];
+  load_q(m, arm, q0 + p * q0_stride, qc, qa);
+  ArmState<T> st;
+  const T nrm = arm_fk_error(m, arm, qc, qa, RT, tT, st);
+  T* o = out + gid * 31;
+  for (int i = 0; i < 9; ++i) o[i] = RT[i];
+  for (int i = 0; i < 3; ++i) o[9 + i] = tT[i];
+  for (int i = 0; i < 9; ++i) o[12 + i] = st.Rh[i];
+  for (int i = 0; i < 3; ++i) o[21 + i] = st.th[i];
+  for (int i = 0; i < 6; ++i) o[24 + i] = st.e[i];
+  o[30] = nrm;
+}
+
+// pin.log6 over a batch of placements (B x 12 -> B x 6).
+template <typename T>
+__global__ __launch_bounds__(256) void ikg_log6_kernel(const T* __restrict__ M, int64_t B, T* __restrict__ out) {
+  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= B) return;
+  T R[9], t[3], e[6];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = M[p * 12 + i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = M[p * 12 + 9 + i];
+  log6(R, t, e);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) out[p * 6 + i] = e[i];
+}
+
 // ------------------------------------------------------------------ launchers
 template <typename T>
 hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
@@ -344,6 +309,30 @@ hipError_t launch_fk(const KModel<T>* dmodel, const void* q, int64_t B, void* ha
   return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_log6(const void* M, int64_t B, void* out, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  constexpr int block = 256;
+  const dim3 grid((unsigned)((B + block - 1) / block));
+  hipLaunchKernelGGL((ikg_log6_kernel<T>), grid, dim3(block), 0, s, (const T*)M, B, (T*)out);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_pair_state(const KModel<T>* dm, const void* targets, const void* q0, int64_t stride, int64_t B,
+                             void* out, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  const dim3 grid((unsigned)((2 * B + 63) / 64));
+  hipLaunchKernelGGL((ikg_pair_state_kernel<T>), grid, dim3(64), 0, s, dm, (const T*)targets, (const T*)q0, stride, B,
+                     (T*)out);
+  return hipGetLastError();
+}
+template hipError_t launch_pair_state<double>(const KModel<double>*, const void*, const void*, int64_t, int64_t,
+                                              void*, hipStream_t);
+template hipError_t launch_pair_state<float>(const KModel<float>*, const void*, const void*, int64_t, int64_t,
+                                             void*, hipStream_t);
+template hipError_t launch_log6<double>(const void*, int64_t, void*, hipStream_t);
+template hipError_t launch_log6<float>(const void*, int64_t, void*, hipStream_t);
 template hipError_t launch_pair_batch<double>(const KModel<double>*, const KParams<double>&, const BatchArgs&,
                                               hipStream_t);
 template hipError_t launch_pair_batch<float>(const KModel<float>*, const KParams<float>&, const BatchArgs&,

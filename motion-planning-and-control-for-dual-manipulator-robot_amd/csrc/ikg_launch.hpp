@@ -40,6 +40,13 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
 template <typename T>
 hipError_t launch_fk(const KModel<T>* dmodel, const void* q, int64_t B, void* hands, hipStream_t s);
 
+template <typename T>
+hipError_t launch_log6(const void* M, int64_t B, void* out, hipStream_t s);
+
+template <typename T>
+hipError_t launch_pair_state(const KModel<T>* dm, const void* targets, const void* q0, int64_t stride, int64_t B,
+                             void* out, hipStream_t s);
+
 constexpr int kMaxSeedsPerBlock = 512;
 
 }  // namespace ikg

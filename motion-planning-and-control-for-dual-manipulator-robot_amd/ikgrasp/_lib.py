@@ -57,7 +57,7 @@ class Params(C.Structure):
 
 EXPORTS = [
     "ikg_model_create", "ikg_model_destroy", "ikg_params_default", "ikg_solve_batch",
-    "ikg_solve_multistart", "ikg_fk_batch", "ikg_last_error", "ikg_version",
+    "ikg_solve_multistart", "ikg_fk_batch", "ikg_log6_batch", "ikg_last_error", "ikg_version",
 ]
 
 _lib = None
@@ -91,6 +91,8 @@ def load() -> C.CDLL:
     lib.ikg_solve_multistart.restype = i32
     lib.ikg_fk_batch.argtypes = [vp, i32, i32, vp, i64, vp, vp, C.c_uint32]
     lib.ikg_fk_batch.restype = i32
+    lib.ikg_log6_batch.argtypes = [i32, i32, vp, i64, vp, vp, C.c_uint32]
+    lib.ikg_log6_batch.restype = i32
     lib.ikg_last_error.argtypes = []
     lib.ikg_last_error.restype = C.c_char_p
     lib.ikg_version.argtypes = []

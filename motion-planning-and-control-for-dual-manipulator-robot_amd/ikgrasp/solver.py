@@ -150,6 +150,16 @@ class IKSolver:
             _lib.IKG_FLAG_HOST_POINTERS))
         return Solution(q_out, conv.astype(bool), iters, err, best)
 
+    # ------------------------------------------------------------------ log6
+    def log6(self, M, dtype="f64") -> np.ndarray:
+        """pin.log6 of placements [B,12] -> [B,6] ([v; w])."""
+        code, npt = _dtype(dtype)
+        mm = np.ascontiguousarray(M, dtype=npt).reshape(-1, 12)
+        out = np.empty((mm.shape[0], 6), dtype=npt)
+        _lib.check(self.lib.ikg_log6_batch(self.device, code, mm.ctypes.data, mm.shape[0], out.ctypes.data, None,
+                                           _lib.IKG_FLAG_HOST_POINTERS))
+        return out
+
     # ------------------------------------------------------------------ FK
     def fk(self, q, dtype="f64") -> np.ndarray:
         """Hands placements [B, 2, 12] (R row-major, t) for q [B, nq]."""
