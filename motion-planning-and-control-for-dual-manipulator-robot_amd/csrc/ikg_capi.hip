@@ -40,6 +40,7 @@ struct ikg_model {
   ikg_model_desc desc;
   ikg::KModel<double> k64;
   ikg::KModel<float> k32;
+  int spec = ikg::kSpecGeneric;
   std::mutex mu;
   std::vector<void*> dev64;  // per device
   std::vector<void*> dev32;
@@ -178,7 +179,7 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
     a.err_out = err_out ? st.out(sizeof(T) * 2 * B) : nullptr;
     if (st.rc) return st.rc;
   }
-  hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, s);
+  hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, model->spec, s);
   if (e != hipSuccess) return hip_fail(e, "ikg pair kernel launch");
   if (host) {
     st.back(q_out, a.q_out, sizeof(T) * nq * B);
@@ -213,7 +214,7 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
     a.best_seed = best_seed ? (int32_t*)st.out(sizeof(int32_t) * T_) : nullptr;
     if (st.rc) return st.rc;
   }
-  hipError_t e = ikg::launch_multistart<T>(dm, kparams<T>(params), a, s);
+  hipError_t e = ikg::launch_multistart<T>(dm, kparams<T>(params), a, model->spec, s);
   if (e != hipSuccess) return hip_fail(e, "ikg multistart kernel launch");
   if (host) {
     st.back(q_out, a.q_out, sizeof(T) * nq * T_);
@@ -364,11 +365,12 @@ int ikg_model_create(const ikg_model_desc* d, ikg_model** out) {
   for (int j = 0; j < IKG_ARM_DOF; ++j)
     if (d->axis[d->arm_q[0][j]] != d->axis[d->arm_q[1][j]])
       return fail(IKG_EINVAL, "arm joint %d: left/right axes differ (unsupported)", j);
-    ikg_model* m = new (std::nothrow) ikg_model();
+  ikg_model* m = new (std::nothrow) ikg_model();
   if (!m) return fail(IKG_ENOMEM, "out of host memory");
   m->desc = *d;
   ikg::build_kmodel<double>(*d, m->k64);
   ikg::build_kmodel<float>(*d, m->k32);
+  m->spec = ikg::choose_spec(m->k64);
   *out = m;
   return IKG_OK;
 }

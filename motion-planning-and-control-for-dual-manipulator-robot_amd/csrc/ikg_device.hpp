@@ -13,6 +13,13 @@
 // exact kernel arithmetic on the CPU for debugging (never a product path).
 #define IKG_HD __host__ __device__
 
+// Timing-only ablation switches (tools/ablate.py builds; never the shipped
+// library): bit 0 = cheap joint sincos, bit 1 = trivial log6,
+// bit 2 = skip the 6x6 solve.
+#ifndef IKG_ABL
+#define IKG_ABL 0
+#endif
+
 namespace ikg {
 
 constexpr int kArmDof = 6;
@@ -43,7 +50,29 @@ struct KModel {
   int32_t arm_axis[kArmDof];
   int32_t nq;
   int32_t rot_mask;  // bit k (k<6): arm joint k placement rotation != I; bit 6: root
+  int32_t hand_axis;  // 0/1/2: hand placement rotation is R_axis(angle) (hand_sc); 3: general
+  T hand_sc[2][2];    // (sin, cos) of that angle per hand
+  int32_t wrist;      // 1: axes of arm joints 3,4,5 meet at the origin of arm joint 4
+  int32_t pattern;    // compile-time specialisation code (ikg_model_build.hpp)
 };
+
+// ---------------------------------------------------------------- kernel specialisation
+// Joint-axis pattern packed 2 bits per slot: slot 0 = root, 1..6 = arm joints,
+// 7 = hand frame rotation; value 3 = "read from the model at run time".
+constexpr int kAxRuntime = 3;
+constexpr int kPatternGeneric = 0xFFFF;
+
+template <int PAT, bool PROT, bool WRIST>
+struct Spec {
+  static constexpr int axis(int slot) { return (PAT >> (2 * slot)) & 3; }
+  static constexpr bool prot = PROT;    // arm joint placements carry rotations
+  static constexpr bool wrist = WRIST;  // decoupled spherical-wrist solve
+};
+using SpecGeneric = Spec<kPatternGeneric, true, false>;
+// Nextage (NextageaOpen.urdf:580-730): root Z; arm Z,Y,Y,X,Y,Z; hand Rz(1.5708);
+// identity joint placements; spherical wrist at LARM/RARM_JOINT4.
+constexpr int kPatternNextage = 2 | (2 << 2) | (1 << 4) | (1 << 6) | (0 << 8) | (1 << 10) | (2 << 12) | (2 << 14);
+using SpecNextage = Spec<kPatternNextage, false, true>;
 
 template <typename T>
 struct KParams {
@@ -166,47 +195,55 @@ IKG_HD inline void column(const T* R, int axis, T* a) {
 }
 
 // ---------------------------------------------------------------- log3 / log6
-// pin.log3 (2.6-era branch structure) and pin.log6 ->
-// [v; w] (inverse_geometry.py:66-67).
+// pin.log3 / pin.log6 -> [v; w] (inverse_geometry.py:66-67), with Pinocchio's
+// branch structure: near-pi diagonal formula for
+// theta >= pi - 1e-2, Taylor series below precision<3>().  The nominal branch
+// is evaluated from sin(theta) = |skew(R)|/2 and cos(theta) = (tr R - 1)/2,
+// which removes three transcendental calls and three divisions from the
+// reference formulas (alpha = theta sin/(2(1-cos)) = theta (1+cos)/(2 sin),
+// beta = 1/theta^2 - sin/(2 theta (1-cos)) = (1-alpha)/theta^2).
 template <typename T>
 IKG_HD inline void log6(const T* R, const T* p, T* e) {
   const T pi = Prec<T>::kPi;
   const T tr = R[0] + R[4] + R[8];
   const T sx = R[7] - R[5], sy = R[2] - R[6], sz = R[3] - R[1];
+  const T ct = (tr - T(1)) * T(0.5);
+  const T st = sqrt(sx * sx + sy * sy + sz * sz) * T(0.5);
   T theta;
   if constexpr (sizeof(T) == 8) {
-    theta = tr > T(3) ? T(0) : (tr < T(-1) ? pi : acos((tr - T(1)) / T(2)));
+    theta = tr > T(3) ? T(0) : (tr < T(-1) ? pi : acos(ct));  // as pin.log3
   } else {
-    // fp32: atan2 of (sin, cos) keeps theta accurate near 0 where acos is not.
-    const T sn = sqrtf(sx * sx + sy * sy + sz * sz) * T(0.5);
-    theta = atan2f(sn, (tr - T(1)) * T(0.5));
+    theta = atan2f(st, ct);  // fp32: accurate near 0 where acos is not
   }
-  T w[3];
+  T w[3], alpha;
+  const T t2 = theta * theta;
   if (theta >= pi - T(1e-2)) {
     T s_, cphi;
     Prec<T>::sincos_(theta - pi, &s_, &cphi);
-    const T beta = theta * theta / (T(1) + cphi);
-    const T t0 = (R[0] + cphi) * beta, t1 = (R[4] + cphi) * beta, t2 = (R[8] + cphi) * beta;
+    const T beta = t2 / (T(1) + cphi);
+    const T t0 = (R[0] + cphi) * beta, t1 = (R[4] + cphi) * beta, tt = (R[8] + cphi) * beta;
     w[0] = (R[7] > R[5] ? T(1) : T(-1)) * (t0 > T(0) ? sqrt(t0) : T(0));
     w[1] = (R[2] > R[6] ? T(1) : T(-1)) * (t1 > T(0) ? sqrt(t1) : T(0));
-    w[2] = (R[3] > R[1] ? T(1) : T(-1)) * (t2 > T(0) ? sqrt(t2) : T(0));
+    w[2] = (R[3] > R[1] ? T(1) : T(-1)) * (tt > T(0) ? sqrt(tt) : T(0));
+    // here sin(theta) from |skew| is inaccurate; 1 - cos(theta) ~ 2 is benign
+    alpha = theta * (-s_) / (T(2) * (T(1) - ct));  // sin(theta) = -sin(theta - pi)
   } else {
     T f;
     if (theta > Prec<T>::kPrec3) {
-      f = theta / sin(theta);
+      f = theta / st;
     } else if constexpr (sizeof(T) == 8) {
       f = T(1);  // Pinocchio: theta/sin(theta) -> 1 below precision<3>()
     } else {
-      const T t2 = theta * theta;
       f = T(1) + t2 * (T(1) / T(6) + t2 * (T(7) / T(360)));
     }
-    f *= T(0.5);
-    w[0] = f * sx;
-    w[1] = f * sy;
-    w[2] = f * sz;
+    const T hf = f * T(0.5);
+    w[0] = hf * sx;
+    w[1] = hf * sy;
+    w[2] = hf * sz;
+    // theta (1+cos)/(2 sin) for cos >= 0, theta sin/(2(1-cos)) otherwise: no cancellation
+    alpha = ct >= T(0) ? hf * (T(1) + ct) : theta * st / (T(2) * (T(1) - ct));
   }
-  T alpha, beta;
-  const T t2 = theta * theta;
+  T beta;
   if (theta < Prec<T>::kPrec3) {
     if constexpr (sizeof(T) == 8) {
       alpha = T(1) - t2 / T(12) - t2 * t2 / T(720);
@@ -216,18 +253,7 @@ IKG_HD inline void log6(const T* R, const T* p, T* e) {
       beta = T(1) / T(12) + t2 * (T(1) / T(720) + t2 * (T(1) / T(30240) + t2 * (T(1) / T(1209600))));
     }
   } else {
-    if constexpr (sizeof(T) == 8) {
-      T st, ct;
-      Prec<T>::sincos_(theta, &st, &ct);
-      alpha = theta * st / (T(2) * (T(1) - ct));
-      beta = T(1) / t2 - st / (T(2) * theta * (T(1) - ct));
-    } else {
-      // half-angle form: no 1-cos cancellation in fp32
-      T sh, ch;
-      Prec<T>::sincos_(theta * T(0.5), &sh, &ch);
-      alpha = theta * T(0.5) * ch / sh;
-      beta = (T(1) - alpha) / t2;
-    }
+    beta = (T(1) - alpha) / t2;
   }
   const T wp = w[0] * p[0] + w[1] * p[1] + w[2] * p[2];
   const T bwp = beta * wp;
@@ -240,63 +266,146 @@ IKG_HD inline void log6(const T* R, const T* p, T* e) {
   e[5] = w[2];
 }
 
+// ---------------------------------------------------------------- joint trigonometry
+// sin/cos of every supporting joint are carried across iterations: after an
+// update q -> q + d the pair is advanced by the angle-addition formula with
+// Taylor series of sin d / cos d (|d| <= kIncMax keeps the truncation below
+// 1e-18 in fp64), and recomputed exactly every kResync iterations, after a
+// large step, or after a clamp.  This replaces 7 sincos calls per lane and
+// iteration of pin.framesForwardKinematics (inverse_geometry.py:58).
+template <typename T>
+struct Trig;
+#ifndef IKG_RESYNC64
+#define IKG_RESYNC64 32
+#endif
+template <>
+struct Trig<double> {
+  static constexpr double kIncMax = 0.1;
+  static constexpr int kResync = IKG_RESYNC64;
+  IKG_HD static inline void step(double d, double& s, double& c) {
+    const double d2 = d * d;
+    const double sd = d + d * d2 * (-1.0 / 6 + d2 * (1.0 / 120 + d2 * (-1.0 / 5040 + d2 * (1.0 / 362880))));
+    const double cd =
+        1.0 + d2 * (-0.5 + d2 * (1.0 / 24 + d2 * (-1.0 / 720 + d2 * (1.0 / 40320 + d2 * (-1.0 / 3628800)))));
+    const double sn = s * cd + c * sd;
+    c = c * cd - s * sd;
+    s = sn;
+  }
+};
+template <>
+struct Trig<float> {
+  static constexpr float kIncMax = 0.1f;
+  static constexpr int kResync = 16;
+  IKG_HD static inline void step(float d, float& s, float& c) {
+    const float d2 = d * d;
+    const float sd = d + d * d2 * (-1.0f / 6 + d2 * (1.0f / 120 + d2 * (-1.0f / 5040)));
+    const float cd = 1.0f + d2 * (-0.5f + d2 * (1.0f / 24 + d2 * (-1.0f / 720)));
+    const float sn = s * cd + c * sd;
+    c = c * cd - s * sd;
+    s = sn;
+  }
+};
+
 // ---------------------------------------------------------------- one arm's kinematics
+template <int AX, typename T>
+IKG_HD inline void rotate_ax(T* R, int runtime_axis, T s, T c) {
+  if constexpr (AX == kAxRuntime)
+    rotate_axis(R, runtime_axis, s, c);
+  else
+    rotate_axis(R, AX, s, c);
+}
+
+template <int AX, typename T>
+IKG_HD inline void column_ax(const T* R, int runtime_axis, T* a) {
+  if constexpr (AX == kAxRuntime)
+    column(R, runtime_axis, a);
+  else
+    column(R, AX, a);
+}
+
 // Forward kinematics of the shared root joint + one arm (pin.forwardKinematics
-// restricted to the hand's support, inverse_geometry.py:58) producing:
+// restricted to the hand's support, inverse_geometry.py:58) given the joints'
+// (sin, cos) (slot 0 = root, 1..6 = arm), producing
 //   Rh, th  : effector frame placement oMf (data.oMf[LARM/RARM_EFF], :62-63)
 //   ax, org : world axis / origin of the 7 supporting joints (root first)
-template <typename T, bool WANT_AXES>
-IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, T qc, const T* qa, T* Rh, T* th,
-                              T (*ax)[3], T (*org)[3]) {
+template <typename T, class SP, bool WANT_AXES>
+IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, T* Rh, T* th,
+                          T (*ax)[3], T (*org)[3]) {
   T R[9], t[3];
-  T s, c;
-  Prec<T>::sincos_(qc, &s, &c);
+  if constexpr (SP::prot) {
 #pragma unroll
-  for (int i = 0; i < 9; ++i) R[i] = m->root_R[i];
+    for (int i = 0; i < 9; ++i) R[i] = m->root_R[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? T(1) : T(0);
+  }
 #pragma unroll
   for (int i = 0; i < 3; ++i) t[i] = m->root_t[i];
-  rotate_axis(R, m->root_axis, s, c);
+  rotate_ax<SP::axis(0)>(R, m->root_axis, sn[0], cs[0]);
   if constexpr (WANT_AXES) {
-    column(R, m->root_axis, ax[0]);
+    column_ax<SP::axis(0)>(R, m->root_axis, ax[0]);
 #pragma unroll
     for (int i = 0; i < 3; ++i) org[0][i] = t[i];
   }
   const bool right = arm != 0;
 #pragma unroll
   for (int k = 0; k < kArmDof; ++k) {
-    T pt[3];
+    T pt[3], dt_[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) pt[i] = sel(right, m->arm_t[1][k][i], m->arm_t[0][k][i]);
-    T dt_[3];
     matvec3(R, pt, dt_);
 #pragma unroll
     for (int i = 0; i < 3; ++i) t[i] += dt_[i];
-    if (m->rot_mask & (1 << k)) {
-      T P[9], Rn[9];
+    if constexpr (SP::prot) {
+      if (m->rot_mask & (1 << k)) {
+        T P[9], Rn[9];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) P[i] = sel(right, m->arm_R[1][k][i], m->arm_R[0][k][i]);
-      matmul3(R, P, Rn);
+        for (int i = 0; i < 9; ++i) P[i] = sel(right, m->arm_R[1][k][i], m->arm_R[0][k][i]);
+        matmul3(R, P, Rn);
 #pragma unroll
-      for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+        for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+      }
     }
-    Prec<T>::sincos_(qa[k], &s, &c);
-    const int axis = m->arm_axis[k];
-    rotate_axis(R, axis, s, c);
+    switch (k) {  // unrolled: k is a compile-time constant after #pragma unroll
+      case 0: rotate_ax<SP::axis(1)>(R, m->arm_axis[0], sn[1], cs[1]); break;
+      case 1: rotate_ax<SP::axis(2)>(R, m->arm_axis[1], sn[2], cs[2]); break;
+      case 2: rotate_ax<SP::axis(3)>(R, m->arm_axis[2], sn[3], cs[3]); break;
+      case 3: rotate_ax<SP::axis(4)>(R, m->arm_axis[3], sn[4], cs[4]); break;
+      case 4: rotate_ax<SP::axis(5)>(R, m->arm_axis[4], sn[5], cs[5]); break;
+      default: rotate_ax<SP::axis(6)>(R, m->arm_axis[5], sn[6], cs[6]); break;
+    }
     if constexpr (WANT_AXES) {
-      column(R, axis, ax[k + 1]);
+      switch (k) {
+        case 0: column_ax<SP::axis(1)>(R, m->arm_axis[0], ax[1]); break;
+        case 1: column_ax<SP::axis(2)>(R, m->arm_axis[1], ax[2]); break;
+        case 2: column_ax<SP::axis(3)>(R, m->arm_axis[2], ax[3]); break;
+        case 3: column_ax<SP::axis(4)>(R, m->arm_axis[3], ax[4]); break;
+        case 4: column_ax<SP::axis(5)>(R, m->arm_axis[4], ax[5]); break;
+        default: column_ax<SP::axis(6)>(R, m->arm_axis[5], ax[6]); break;
+      }
 #pragma unroll
       for (int i = 0; i < 3; ++i) org[k + 1][i] = t[i];
     }
   }
-  T ht[3], hR[9], d[3];
+  T ht[3], d[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) ht[i] = sel(right, m->hand_t[1][i], m->hand_t[0][i]);
-#pragma unroll
-  for (int i = 0; i < 9; ++i) hR[i] = sel(right, m->hand_R[1][i], m->hand_R[0][i]);
   matvec3(R, ht, d);
 #pragma unroll
   for (int i = 0; i < 3; ++i) th[i] = t[i] + d[i];
-  matmul3(R, hR, Rh);
+  constexpr int HA = SP::axis(7);
+  if constexpr (HA != kAxRuntime) {
+    // hand placement rotation = R_axis(angle): two columns change
+#pragma unroll
+    for (int i = 0; i < 9; ++i) Rh[i] = R[i];
+    rotate_axis(Rh, HA, sel(right, m->hand_sc[1][0], m->hand_sc[0][0]),
+                sel(right, m->hand_sc[1][1], m->hand_sc[0][1]));
+  } else {
+    T hR[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) hR[i] = sel(right, m->hand_R[1][i], m->hand_R[0][i]);
+    matmul3(R, hR, Rh);
+  }
 }
 
 // log6(oMhand^-1 * oMtarget) (inverse_geometry.py:66-67)
@@ -307,7 +416,12 @@ IKG_HD inline void pose_error(const T* Rh, const T* th, const T* RT, const T* tT
 #pragma unroll
   for (int i = 0; i < 3; ++i) d[i] = tT[i] - th[i];
   matvec3_t(Rh, d, pm);
-  log6(Rm, pm, e);
+  if constexpr (IKG_ABL & 2) {
+    e[0] = pm[0]; e[1] = pm[1]; e[2] = pm[2];
+    e[3] = T(0.5) * (Rm[7] - Rm[5]); e[4] = T(0.5) * (Rm[2] - Rm[6]); e[5] = T(0.5) * (Rm[3] - Rm[1]);
+  } else {
+    log6(Rm, pm, e);
+  }
 }
 
 // ---------------------------------------------------------------- 6x6 solve, 2 RHS
@@ -409,19 +523,47 @@ IKG_HD inline T clampq(T q, T lo, T hi) {
 // ---------------------------------------------------------------- per-lane iteration stages
 // One arm-lane's share of an iteration of inverse_geometry.py:56-89.  The
 // kernel composes these with DPP exchanges (ikg_kernels.hip solve_pair);
-// tools/host_emu.cpp composes the same functions for both arms on the CPU.
+// tools/host_emu (ikg_host_emu.hip) composes the same functions for both arms
+// on the CPU.
 template <typename T>
 struct ArmState {
-  T Rh[9], th[3];       // effector placement oMf
+  T Rh[9], th[3];         // effector placement oMf
   T ax[7][3], org[7][3];  // world axis / origin of root + arm joints
-  T e[6];               // log6(oMf^-1 oMtarget)
+  T e[6];                 // log6(oMf^-1 oMtarget)
 };
 
-// FK + pose error; returns |e| (inverse_geometry.py:58-67).
+// exact (sin, cos) of the root and arm joints (slot 0 = root)
 template <typename T>
-IKG_HD inline T arm_fk_error(const KModel<T>* __restrict__ m, int arm, T qc, const T* qa, const T* RT, const T* tT,
-                             ArmState<T>& st) {
-  fk_arm<T, true>(m, arm, qc, qa, st.Rh, st.th, st.ax, st.org);
+IKG_HD inline void trig_exact(T qc, const T* qa, T* sn, T* cs) {
+  Prec<T>::sincos_(qc, &sn[0], &cs[0]);
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) Prec<T>::sincos_(qa[k], &sn[k + 1], &cs[k + 1]);
+}
+
+// advance (sin, cos) after the update q_old -> (qc, qa); exact when `resync`
+// or when any step exceeds the incremental range
+template <typename T>
+IKG_HD inline void trig_advance(T qc, const T* qa, const T* q_old, bool resync, T* sn, T* cs) {
+  T d[7];
+  d[0] = qc - q_old[0];
+  bool big = resync;
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) d[k + 1] = qa[k] - q_old[k + 1];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) big |= fabs(d[j]) > Trig<T>::kIncMax;
+  if (big) {
+    trig_exact(qc, qa, sn, cs);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
+  }
+}
+
+// FK + pose error; returns |e| (inverse_geometry.py:58-67).
+template <typename T, class SP>
+IKG_HD inline T arm_fk_error(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, const T* RT,
+                             const T* tT, ArmState<T>& st) {
+  fk_arm<T, SP, true>(m, arm, sn, cs, st.Rh, st.th, st.ax, st.org);
   pose_error(st.Rh, st.th, RT, tT, st.e);
   const T* e = st.e;
   return sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3] + e[4] * e[4] + e[5] * e[5]);
@@ -454,10 +596,89 @@ IKG_HD inline void arm_system(const ArmState<T>& st, T (&A)[6][8]) {
   }
 }
 
-// lambda = 0: u = J_a^-1 e_a, v = J_a^-1 c_a; alpha = u.v, beta = v.v.
 template <typename T>
-IKG_HD inline void arm_solve(T (&A)[6][8], T* u, T* v, T& alpha, T& beta) {
-  qr_solve6(A, u, v);
+IKG_HD inline void cross3(const T* a, const T* b, T* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+template <typename T>
+IKG_HD inline T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+
+// [g1 g2 g3]^-1 applied to b0 and b1 by the adjugate (Cramer); a determinant
+// below rcond * |g1||g2||g3| truncates the inverse to zero (pinv's rcond).
+template <typename T>
+IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b0, const T* b1, T* x0, T* x1) {
+  T r1[3], r2[3], r3[3];
+  cross3(g2, g3, r1);
+  cross3(g3, g1, r2);
+  cross3(g1, g2, r3);
+  const T det = dot3(g1, r1);
+  const T bound = dot3(g1, g1) * dot3(g2, g2) * dot3(g3, g3);
+  const T rc = Prec<T>::kRcond;
+  const T rdet = det * det > rc * rc * bound ? T(1) / det : T(0);
+  x0[0] = dot3(r1, b0) * rdet;
+  x0[1] = dot3(r2, b0) * rdet;
+  x0[2] = dot3(r3, b0) * rdet;
+  x1[0] = dot3(r1, b1) * rdet;
+  x1[1] = dot3(r2, b1) * rdet;
+  x1[2] = dot3(r3, b1) * rdet;
+}
+
+// Spherical wrist (axes of arm joints 3,4,5 through w = origin of arm joint 4):
+// written at w the square arm Jacobian is block lower-triangular,
+//   [ G  0 ] with G = [a_j x (w - o_j)]_{j=0..2},  H = [a_j]_{j=3..5},
+//   [ F  H ]      F = [a_j]_{j=0..2},
+// so J_a^-1 [e c] needs two 3x3 solves.  Rows are moved from the hand point h
+// to w by v_w = v_h + w_ang x (w - h) (an invertible row operation: same u, v).
+template <typename T>
+IKG_HD inline void arm_solve_wrist(const ArmState<T>& st, T* u, T* v) {
+  const T* w = st.org[5];
+  T ev[3], ew[3], bl[3], wh[3], tmp[3];
+  matvec3(st.Rh, st.e, ev);
+  matvec3(st.Rh, st.e + 3, ew);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) wh[i] = w[i] - st.th[i];
+  cross3(ew, wh, tmp);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) bl[i] = ev[i] + tmp[i];
+  T g[3][3], cl[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    T ow[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ow[i] = w[i] - st.org[j + 1][i];
+    cross3(st.ax[j + 1], ow, g[j]);
+  }
+  {
+    T ow[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ow[i] = w[i] - st.org[0][i];
+    cross3(st.ax[0], ow, cl);
+  }
+  inv3_apply2(g[0], g[1], g[2], bl, cl, u, v);
+  T re[3], rcv[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    re[i] = ew[i] - (u[0] * st.ax[1][i] + u[1] * st.ax[2][i] + u[2] * st.ax[3][i]);
+    rcv[i] = st.ax[0][i] - (v[0] * st.ax[1][i] + v[1] * st.ax[2][i] + v[2] * st.ax[3][i]);
+  }
+  inv3_apply2(st.ax[4], st.ax[5], st.ax[6], re, rcv, u + 3, v + 3);
+}
+
+// lambda = 0: u = J_a^-1 e_a, v = J_a^-1 c_a; alpha = u.v, beta = v.v.
+template <typename T, class SP>
+IKG_HD inline void arm_solve(const ArmState<T>& st, T* u, T* v, T& alpha, T& beta) {
+  if constexpr (IKG_ABL & 4) {
+    for (int k = 0; k < 6; ++k) { u[k] = st.e[k] + st.org[k][0]; v[k] = st.ax[k][1]; }
+  } else if constexpr (SP::wrist) {
+    arm_solve_wrist(st, u, v);
+  } else {
+    T A[6][8];
+    arm_system(st, A);
+    qr_solve6(A, u, v);
+  }
   alpha = T(0);
   beta = T(0);
 #pragma unroll
@@ -533,6 +754,4 @@ IKG_HD inline void arm_update(const KModel<T>* __restrict__ m, int arm, T dt, T 
     qa[k] = clampq(qa[k] + dq[k] * dt, lo, hi);
   }
 }
-
-
 }  // namespace ikg

@@ -12,11 +12,11 @@
 
 namespace {
 
-template <typename T>
+template <typename T, class SP>
 void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, const T* tg, const T* qrow,
              T* qo, uint8_t* conv_out, int32_t* iters_out, T* err_out, T* trace, int trace_len) {
   using namespace ikg;
-  T RT[2][9], tT[2][3], qc[2], qa[2][kArmDof];
+  T RT[2][9], tT[2][3], qc[2], qa[2][kArmDof], sn[2][7], cs[2][7];
   for (int arm = 0; arm < 2; ++arm) {
     const bool right = arm != 0;
     T HR[9], Ht[3], d[3];
@@ -27,13 +27,15 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
     for (int i = 0; i < 3; ++i) tT[arm][i] = tg[9 + i] + d[i];
     qc[arm] = qrow[m.root_q];
     for (int k = 0; k < kArmDof; ++k) qa[arm][k] = qrow[m.arm_q[arm][k]];
+    trig_exact(qc[arm], qa[arm], sn[arm], cs[arm]);
   }
   int it = 0;
   bool conv = false;
   T nrm[2];
   for (;;) {
     ArmState<T> st[2];
-    for (int arm = 0; arm < 2; ++arm) nrm[arm] = arm_fk_error(&m, arm, qc[arm], qa[arm], RT[arm], tT[arm], st[arm]);
+    for (int arm = 0; arm < 2; ++arm)
+      nrm[arm] = arm_fk_error<T, SP>(&m, arm, sn[arm], cs[arm], RT[arm], tT[arm], st[arm]);
     if (trace && it < trace_len) {
       trace[2 * it] = nrm[0];
       trace[2 * it + 1] = nrm[1];
@@ -43,14 +45,18 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
       conv = true;
       break;
     }
-    T A[2][6][8], u[2][6], v[2][6], al[2], be[2], dq[6];
+    T A[2][6][8], u[2][6], v[2][6], al[2], be[2], dq[6], q_old[2][7];
     for (int arm = 0; arm < 2; ++arm) {
-      arm_system(st[arm], A[arm]);
-      if (damped)
+      q_old[arm][0] = qc[arm];
+      for (int k = 0; k < kArmDof; ++k) q_old[arm][k + 1] = qa[arm][k];
+      if (damped) {
+        arm_system(st[arm], A[arm]);
         arm_solve_damped(A[arm], prm.lambda, u[arm], v[arm], al[arm], be[arm]);
-      else
-        arm_solve(A[arm], u[arm], v[arm], al[arm], be[arm]);
+      } else {
+        arm_solve<T, SP>(st[arm], u[arm], v[arm], al[arm], be[arm]);
+      }
     }
+    ++it;
     for (int arm = 0; arm < 2; ++arm) {
       const T s = chest_step(al[arm] + al[1 - arm], be[arm] + be[1 - arm]);
       if (damped)
@@ -58,8 +64,8 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
       else
         arm_dq(u[arm], v[arm], s, dq);
       arm_update(&m, arm, prm.dt, s, dq, qc[arm], qa[arm]);
+      trig_advance(qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
     }
-    ++it;
   }
   for (int j = 0; j < m.nq; ++j) qo[j] = qrow[j];
   for (int i = 0; i < m.n_passive; ++i) {
@@ -81,10 +87,18 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
   ikg::KModel<T> m;
   ikg::build_kmodel<T>(*d, m);
   ikg::KParams<T> prm{(T)p->eps, (T)p->dt, (T)p->lambda, p->max_iters};
-  for (int64_t i = 0; i < B; ++i)
-    emu_one<T>(m, prm, p->lambda > 0, (const T*)targets + 12 * i, (const T*)q0 + stride * i,
-               (T*)q_out + d->nq * i, conv + i, iters + i, (T*)err + 2 * i,
-               trace ? (T*)trace + (int64_t)2 * trace_len * i : nullptr, trace_len);
+  const bool special = p->variant != 99 && ikg::choose_spec(m) == 1;  // variant 99: force generic
+  for (int64_t i = 0; i < B; ++i) {
+    const T* tg = (const T*)targets + 12 * i;
+    const T* qr = (const T*)q0 + stride * i;
+    T* tr = trace ? (T*)trace + (int64_t)2 * trace_len * i : nullptr;
+    if (special)
+      emu_one<T, ikg::SpecNextage>(m, prm, p->lambda > 0, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
+                                   (T*)err + 2 * i, tr, trace_len);
+    else
+      emu_one<T, ikg::SpecGeneric>(m, prm, p->lambda > 0, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
+                                   (T*)err + 2 * i, tr, trace_len);
+  }
 }
 
 }  // namespace

@@ -27,39 +27,44 @@ namespace ikg {
 // One problem, one arm: run the reference loop to its stop condition.
 // Returns (through refs) the final q of this lane, the update count and the
 // norm of this lane's hand error at the returned q.
-template <typename T, bool DAMPED>
+template <typename T, bool DAMPED, class SP>
 __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, const T* RT,
                                   const T* tT, T& qc, T* qa, int& it_out, bool& conv_out, T& nrm_out,
                                   T& other_out) {
+  T sn[7], cs[7];
+  trig_exact(qc, qa, sn, cs);
   int it = 0;
   bool conv = false;
   T nrm, other;
   for (;;) {
     ArmState<T> st;
-    nrm = arm_fk_error(m, arm, qc, qa, RT, tT, st);
+    nrm = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
     other = pair_swap(nrm);
     if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
     if (nrm < prm.eps && other < prm.eps) {
       conv = true;
       break;
     }
-    T A[6][8];
-    arm_system(st, A);
-    T dq[6], alpha, beta;
+    T q_old[7];
+    q_old[0] = qc;
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
+    T dq[6], alpha, beta, s;
     if constexpr (!DAMPED) {
       T u[6], v[6];
-      arm_solve(A, u, v, alpha, beta);
-      const T s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+      arm_solve<T, SP>(st, u, v, alpha, beta);
+      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
       arm_dq(u, v, s, dq);
-      arm_update(m, arm, prm.dt, s, dq, qc, qa);
     } else {
-      T ze[6], zc[6];
+      T A[6][8], ze[6], zc[6];
+      arm_system(st, A);
       arm_solve_damped(A, prm.lambda, ze, zc, alpha, beta);
-      const T s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
       arm_dq_damped(A, ze, zc, s, dq);
-      arm_update(m, arm, prm.dt, s, dq, qc, qa);
     }
+    arm_update(m, arm, prm.dt, s, dq, qc, qa);
     ++it;
+    trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }
   it_out = it;
   conv_out = conv;
@@ -113,7 +118,7 @@ __device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T
   for (int k = 0; k < kArmDof; ++k) qo[right ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
 }
 
-template <typename T, bool DAMPED>
+template <typename T, bool DAMPED, class SP>
 __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                                                             const T* __restrict__ targets,
                                                             const T* __restrict__ q0, int64_t q0_stride, int64_t B,
@@ -132,7 +137,7 @@ __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __r
   int it;
   bool conv;
   T nrm, other;
-  solve_pair<T, DAMPED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
+  solve_pair<T, DAMPED, SP>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
   store_q(m, arm, qrow, it, qc, qa, q_out + p * m->nq);
   if (arm == 0) {
     if (conv_out) conv_out[p] = conv ? 1 : 0;
@@ -143,7 +148,7 @@ __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __r
 
 // Multi-start: one workgroup per target, seed i on lanes (2i, 2i+1); the
 // best seed is reduced in LDS inside the workgroup (no cross-GPU traffic).
-template <typename T, bool DAMPED>
+template <typename T, bool DAMPED, class SP>
 __global__ __launch_bounds__(1024) void ikg_multistart_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                                                               const T* __restrict__ targets,
                                                               const T* __restrict__ seeds, int64_t S,
@@ -172,7 +177,7 @@ __global__ __launch_bounds__(1024) void ikg_multistart_kernel(const KModel<T>* _
     T RT[9], tT[3];
     hook_target(m, arm, targets + tgt * 12, RT, tT);
     load_q(m, arm, qrow, qc, qa);
-    solve_pair<T, DAMPED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
+    solve_pair<T, DAMPED, SP>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
   }
   __syncthreads();
   // key: converged seeds rank by the worse hand error; unconverged ones after
@@ -214,9 +219,10 @@ __global__ __launch_bounds__(256) void ikg_fk_kernel(const KModel<T>* __restrict
   const T* qrow = q + p * m->nq;
 #pragma unroll 1
   for (int arm = 0; arm < 2; ++arm) {
-    T qc, qa[kArmDof], Rh[9], th[3];
+    T qc, qa[kArmDof], Rh[9], th[3], sn[7], cs[7];
     load_q(m, arm, qrow, qc, qa);
-    fk_arm<T, false>(m, arm, qc, qa, Rh, th, nullptr, nullptr);
+    trig_exact(qc, qa, sn, cs);
+    fk_arm<T, SpecGeneric, false>(m, arm, sn, cs, Rh, th, nullptr, nullptr);
     T* out = hands + p * 24 + arm * 12;
 #pragma unroll
     for (int i = 0; i < 9; ++i) out[i] = Rh[i];
@@ -238,10 +244,11 @@ __global__ __launch_bounds__(64) void ikg_pair_state_kernel(const KModel<T>* __r
   if (p >= B) return;
   T RT[9], tT[3];
   hook_target(m, arm, targets + p * 12, RT, tT);
-  T qc, qa[kArmDof];
+  T qc, qa[kArmDof], sn[7], cs[7];
   load_q(m, arm, q0 + p * q0_stride, qc, qa);
+  trig_exact(qc, qa, sn, cs);
   ArmState<T> st;
-  const T nrm = arm_fk_error(m, arm, qc, qa, RT, tT, st);
+  const T nrm = arm_fk_error<T, SpecGeneric>(m, arm, sn, cs, RT, tT, st);
   T* o = out + gid * 31;
   for (int i = 0; i < 9; ++i) o[i] = RT[i];
   for (int i = 0; i < 3; ++i) o[9 + i] = tT[i];
@@ -267,36 +274,60 @@ __global__ __launch_bounds__(256) void ikg_log6_kernel(const T* __restrict__ M, 
 }
 
 // ------------------------------------------------------------------ launchers
-template <typename T>
-hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
-  if (a.B <= 0) return hipSuccess;
+template <typename T, bool DAMPED, class SP>
+static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
   constexpr int block = 64;
   const int64_t threads = a.B * 2;
   const dim3 grid((unsigned)((threads + block - 1) / block));
-  if (prm.lambda > T(0))
-    hipLaunchKernelGGL((ikg_pair_batch_kernel<T, true>), grid, dim3(block), 0, s, dmodel, prm,
-                       (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, (T*)a.q_out, a.converged, a.iters,
-                       (T*)a.err_out);
-  else
-    hipLaunchKernelGGL((ikg_pair_batch_kernel<T, false>), grid, dim3(block), 0, s, dmodel, prm,
-                       (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, (T*)a.q_out, a.converged, a.iters,
-                       (T*)a.err_out);
-  return hipGetLastError();
+  hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP>), grid, dim3(block), 0, s, dmodel, prm,
+                     (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, (T*)a.q_out, a.converged, a.iters,
+                     (T*)a.err_out);
 }
 
 template <typename T>
-hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, hipStream_t s) {
-  if (a.T <= 0) return hipSuccess;
+hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,
+                             hipStream_t s) {
+  if (a.B <= 0) return hipSuccess;
+  const bool damped = prm.lambda > T(0);
+  if (spec == kSpecNextage) {
+    if (damped)
+      launch_pair_batch_t<T, true, SpecNextage>(dmodel, prm, a, s);
+    else
+      launch_pair_batch_t<T, false, SpecNextage>(dmodel, prm, a, s);
+  } else {
+    if (damped)
+      launch_pair_batch_t<T, true, SpecGeneric>(dmodel, prm, a, s);
+    else
+      launch_pair_batch_t<T, false, SpecGeneric>(dmodel, prm, a, s);
+  }
+  return hipGetLastError();
+}
+
+template <typename T, bool DAMPED, class SP>
+static void launch_multistart_t(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, hipStream_t s) {
   const int block = (int)(((a.S * 2) + 63) / 64 * 64);
   const dim3 grid((unsigned)a.T);
-  if (prm.lambda > T(0))
-    hipLaunchKernelGGL((ikg_multistart_kernel<T, true>), grid, dim3(block), 0, s, dmodel, prm,
-                       (const T*)a.targets, (const T*)a.seeds, a.S, (T*)a.q_out, a.converged, a.iters,
-                       (T*)a.err_out, a.best_seed);
-  else
-    hipLaunchKernelGGL((ikg_multistart_kernel<T, false>), grid, dim3(block), 0, s, dmodel, prm,
-                       (const T*)a.targets, (const T*)a.seeds, a.S, (T*)a.q_out, a.converged, a.iters,
-                       (T*)a.err_out, a.best_seed);
+  hipLaunchKernelGGL((ikg_multistart_kernel<T, DAMPED, SP>), grid, dim3(block), 0, s, dmodel, prm,
+                     (const T*)a.targets, (const T*)a.seeds, a.S, (T*)a.q_out, a.converged, a.iters,
+                     (T*)a.err_out, a.best_seed);
+}
+
+template <typename T>
+hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, int spec,
+                             hipStream_t s) {
+  if (a.T <= 0) return hipSuccess;
+  const bool damped = prm.lambda > T(0);
+  if (spec == kSpecNextage) {
+    if (damped)
+      launch_multistart_t<T, true, SpecNextage>(dmodel, prm, a, s);
+    else
+      launch_multistart_t<T, false, SpecNextage>(dmodel, prm, a, s);
+  } else {
+    if (damped)
+      launch_multistart_t<T, true, SpecGeneric>(dmodel, prm, a, s);
+    else
+      launch_multistart_t<T, false, SpecGeneric>(dmodel, prm, a, s);
+  }
   return hipGetLastError();
 }
 
@@ -333,13 +364,13 @@ template hipError_t launch_pair_state<float>(const KModel<float>*, const void*, 
                                              void*, hipStream_t);
 template hipError_t launch_log6<double>(const void*, int64_t, void*, hipStream_t);
 template hipError_t launch_log6<float>(const void*, int64_t, void*, hipStream_t);
-template hipError_t launch_pair_batch<double>(const KModel<double>*, const KParams<double>&, const BatchArgs&,
+template hipError_t launch_pair_batch<double>(const KModel<double>*, const KParams<double>&, const BatchArgs&, int,
                                               hipStream_t);
-template hipError_t launch_pair_batch<float>(const KModel<float>*, const KParams<float>&, const BatchArgs&,
+template hipError_t launch_pair_batch<float>(const KModel<float>*, const KParams<float>&, const BatchArgs&, int,
                                              hipStream_t);
-template hipError_t launch_multistart<double>(const KModel<double>*, const KParams<double>&, const MultiArgs&,
+template hipError_t launch_multistart<double>(const KModel<double>*, const KParams<double>&, const MultiArgs&, int,
                                               hipStream_t);
-template hipError_t launch_multistart<float>(const KModel<float>*, const KParams<float>&, const MultiArgs&,
+template hipError_t launch_multistart<float>(const KModel<float>*, const KParams<float>&, const MultiArgs&, int,
                                              hipStream_t);
 template hipError_t launch_fk<double>(const KModel<double>*, const void*, int64_t, void*, hipStream_t);
 template hipError_t launch_fk<float>(const KModel<float>*, const void*, int64_t, void*, hipStream_t);

@@ -31,11 +31,17 @@ struct MultiArgs {
   int32_t* best_seed;
 };
 
-template <typename T>
-hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s);
+// kernel specialisation chosen at model creation (ikg_model_build.hpp)
+constexpr int kSpecGeneric = 0;
+constexpr int kSpecNextage = 1;
 
 template <typename T>
-hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, hipStream_t s);
+hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,
+                             hipStream_t s);
+
+template <typename T>
+hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, int spec,
+                             hipStream_t s);
 
 template <typename T>
 hipError_t launch_fk(const KModel<T>* dmodel, const void* q, int64_t B, void* hands, hipStream_t s);

@@ -56,6 +56,49 @@ inline void build_kmodel(const ikg_model_desc& d, KModel<T>& k) {
   k.n_passive = 0;
   for (int q = 0; q < d.nq; ++q)
     if (!used[q]) k.passive_q[k.n_passive++] = q;
+  if (!is_identity(d.placement[r])) k.rot_mask |= 1 << 6;
+
+  // hand frame rotation: a principal-axis rotation R_a(angle) shared by both hands?
+  k.hand_axis = 3;
+  for (int ax = 0; ax < 3 && k.hand_axis == 3; ++ax) {
+    const int b = (ax + 1) % 3, c = (ax + 2) % 3;
+    bool ok = true;
+    for (int h = 0; h < 2; ++h) {
+      const double* R = d.hand[h];
+      auto at = [&](int i, int j) { return R[3 * i + j]; };
+      ok = ok && at(ax, ax) == 1.0 && at(ax, b) == 0.0 && at(ax, c) == 0.0 && at(b, ax) == 0.0 &&
+           at(c, ax) == 0.0 && at(b, b) == at(c, c) && at(b, c) == -at(c, b);
+    }
+    if (ok) {
+      k.hand_axis = ax;
+      for (int h = 0; h < 2; ++h) {
+        k.hand_sc[h][0] = (T)d.hand[h][3 * c + b];  // sin
+        k.hand_sc[h][1] = (T)d.hand[h][3 * b + b];  // cos
+      }
+    }
+  }
+  // spherical wrist: joint 4's origin on joint 3's axis, joint 5's axis
+  // through joint 4's origin (identity placement rotations)
+  k.wrist = 1;
+  for (int a = 0; a < 2; ++a) {
+    const int q3 = d.arm_q[a][3], q4 = d.arm_q[a][4], q5 = d.arm_q[a][5];
+    if (!is_identity(d.placement[q4]) || !is_identity(d.placement[q5])) k.wrist = 0;
+    for (int i = 0; i < 3; ++i) {
+      if (i != d.axis[q3] && d.placement[q4][9 + i] != 0.0) k.wrist = 0;
+      if (i != d.axis[q5] && d.placement[q5][9 + i] != 0.0) k.wrist = 0;
+    }
+  }
+  int pat = d.axis[r];
+  for (int j = 0; j < IKG_ARM_DOF; ++j) pat |= d.axis[d.arm_q[0][j]] << (2 * (j + 1));
+  pat |= k.hand_axis << 14;
+  k.pattern = pat;
+}
+
+// The compiled specialisation this model can use (ikg_launch.hpp kSpec*).
+template <typename T>
+inline int choose_spec(const KModel<T>& k) {
+  if (k.pattern == kPatternNextage && k.rot_mask == 0 && k.wrist) return 1;  // kSpecNextage
+  return 0;                                                                   // kSpecGeneric
 }
 
 

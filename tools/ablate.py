@@ -1,0 +1,56 @@
+"""Interleaved timing of ablation builds (tools/build_ablations.sh) in ONE
+process: B targets, fixed 1000 iterations (eps=1e-37), kernel time by HIP events."""
+import ctypes as C
+import glob
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd"))
+from ikgrasp import _lib  # noqa: E402
+from ikgrasp.model import load_nextage  # noqa: E402
+from ikgrasp.workload import uniform_targets  # noqa: E402
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+dtype = sys.argv[2] if len(sys.argv) > 2 else "f64"
+pattern = sys.argv[3] if len(sys.argv) > 3 else os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd/ikgrasp/_native/abl/*.so")
+libs = sorted(glob.glob(pattern))
+dev = torch.device("cuda", 0)
+tdt = torch.float64 if dtype == "f64" else torch.float32
+code = 0 if dtype == "f64" else 1
+tg = torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device=dev)
+q0 = torch.zeros(15, dtype=tdt, device=dev)
+qo = torch.empty((B, 15), dtype=tdt, device=dev)
+cv = torch.empty(B, dtype=torch.uint8, device=dev)
+it = torch.empty(B, dtype=torch.int32, device=dev)
+er = torch.empty((B, 2), dtype=tdt, device=dev)
+desc = _lib.model_desc(load_nextage())
+handles = []
+for p in libs:
+    lib = C.CDLL(p)
+    lib.ikg_model_create.argtypes = [C.POINTER(_lib.ModelDesc), C.POINTER(C.c_void_p)]
+    lib.ikg_solve_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                    C.POINTER(_lib.Params), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_uint32]
+    h = C.c_void_p()
+    assert lib.ikg_model_create(C.byref(desc), C.byref(h)) == 0
+    handles.append((os.path.basename(p), lib, h))
+prm = _lib.Params(eps=float(os.environ.get("ABL_EPS", "1e-37")), dt=1e-2, max_iters=1000, variant=0, lambda_=0.0)
+s = torch.cuda.current_stream().cuda_stream
+times = {n: [] for n, _, _ in handles}
+for rnd in range(6):
+    for n, lib, h in handles:
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        rc = lib.ikg_solve_batch(h, 0, code, tg.data_ptr(), q0.data_ptr(), 0, B, C.byref(prm), qo.data_ptr(),
+                                 cv.data_ptr(), it.data_ptr(), er.data_ptr(), C.c_void_p(s), 0)
+        b.record()
+        torch.cuda.synchronize()
+        assert rc == 0
+        if rnd > 0:
+            times[n].append(a.elapsed_time(b))
+for n, t in times.items():
+    print(f"{n:30s} B={B} {dtype}: median {np.median(t):.3f} ms  min {np.min(t):.3f}  ({np.median(t) / 1000 * 1e3:.2f} us/iter)")
