@@ -81,6 +81,8 @@ typedef struct ikg_params {
   int32_t max_iters;   /* joint updates before giving up (1000) */
   int32_t variant;     /* enum ikg_variant */
   double lambda;       /* damping of (J J^T + lambda I); 0 = pinv semantics (reference) */
+  int32_t problems_per_wave; /* 1..32 problems per 64-lane wave; 0 = auto (32) */
+  int32_t reserved;
 } ikg_params;
 
 typedef struct ikg_model ikg_model;

@@ -137,6 +137,11 @@ struct Staging {
   }
 };
 
+// Problems per wave.  Full 32-problem waves are fastest at every batch size
+// measured (B = 4k..131k, fp32/fp64): spreading a small batch over more,
+// sparser waves was 1.3-3x SLOWER (profiles/r01/ppw_sweep.txt).
+int auto_ppw(int /*device*/, int64_t /*B*/) { return 32; }
+
 int check_params(const ikg_params* p) {
   if (!p) return fail(IKG_EINVAL, "params is NULL");
   if (!(p->eps > 0) || !std::isfinite(p->eps)) return fail(IKG_EINVAL, "eps must be > 0");
@@ -145,6 +150,8 @@ int check_params(const ikg_params* p) {
   if (!(p->lambda >= 0) || !std::isfinite(p->lambda)) return fail(IKG_EINVAL, "lambda must be >= 0");
   if (p->variant != IKG_VARIANT_AUTO && p->variant != IKG_VARIANT_PAIR)
     return fail(IKG_EINVAL, "variant %d not available in this build", p->variant);
+  if (p->problems_per_wave < 0 || p->problems_per_wave > 32)
+    return fail(IKG_EINVAL, "problems_per_wave must be in [0, 32]");
   return IKG_OK;
 }
 
@@ -166,7 +173,8 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   int rc = model->device_tables<T>(device, &dm);
   if (rc) return rc;
   const int nq = model->desc.nq;
-  ikg::BatchArgs a{targets, q0, q0_stride, B, q_out, converged, iters, err_out};
+  ikg::BatchArgs a{targets, q0, q0_stride, B, q_out, converged, iters, err_out, 32};
+  a.ppw = params->problems_per_wave > 0 ? params->problems_per_wave : auto_ppw(device, B);
   Staging st(s);
   const bool host = flags & IKG_FLAG_HOST_POINTERS;
   if (host) {
@@ -335,6 +343,8 @@ void ikg_params_default(ikg_params* p) {
   p->max_iters = 1000;  // inverse_geometry.py:53
   p->variant = IKG_VARIANT_AUTO;
   p->lambda = 0.0;      // np.linalg.pinv semantics
+  p->problems_per_wave = 0;
+  p->reserved = 0;
 }
 
 int ikg_model_create(const ikg_model_desc* d, ikg_model** out) {

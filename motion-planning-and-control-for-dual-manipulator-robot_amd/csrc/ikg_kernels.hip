@@ -118,17 +118,21 @@ __device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T
   for (int k = 0; k < kArmDof; ++k) qo[right ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
 }
 
+// One 64-lane wave per workgroup holding `ppw` problems on lanes [0, 2 ppw).
+// A wave's issue cost does not depend on how many lanes are active, so small
+// batches are spread with ppw < 32 to occupy every SIMD.
 template <typename T, bool DAMPED, class SP>
 __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                                                             const T* __restrict__ targets,
                                                             const T* __restrict__ q0, int64_t q0_stride, int64_t B,
-                                                            T* __restrict__ q_out, uint8_t* __restrict__ conv_out,
+                                                            int ppw, T* __restrict__ q_out,
+                                                            uint8_t* __restrict__ conv_out,
                                                             int32_t* __restrict__ iters_out,
                                                             T* __restrict__ err_out) {
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t p = gid >> 1;
-  const int arm = (int)(gid & 1);
-  if (p >= B) return;  // both lanes of a pair leave together
+  const int lane = threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
+  const int arm = lane & 1;
+  if (lane >= 2 * ppw || p >= B) return;  // both lanes of a pair leave together
   T RT[9], tT[3];
   hook_target(m, arm, targets + p * 12, RT, tT);
   const T* qrow = q0 + p * q0_stride;
@@ -276,12 +280,11 @@ __global__ __launch_bounds__(256) void ikg_log6_kernel(const T* __restrict__ M, 
 // ------------------------------------------------------------------ launchers
 template <typename T, bool DAMPED, class SP>
 static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
-  constexpr int block = 64;
-  const int64_t threads = a.B * 2;
-  const dim3 grid((unsigned)((threads + block - 1) / block));
-  hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP>), grid, dim3(block), 0, s, dmodel, prm,
-                     (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, (T*)a.q_out, a.converged, a.iters,
-                     (T*)a.err_out);
+  const int ppw = a.ppw;
+  const dim3 grid((unsigned)((a.B + ppw - 1) / ppw));
+  hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP>), grid, dim3(64), 0, s, dmodel, prm,
+                     (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, ppw, (T*)a.q_out, a.converged,
+                     a.iters, (T*)a.err_out);
 }
 
 template <typename T>

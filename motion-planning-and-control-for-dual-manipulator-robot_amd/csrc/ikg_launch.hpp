@@ -17,6 +17,7 @@ struct BatchArgs {
   uint8_t* converged;
   int32_t* iters;
   void* err_out;
+  int ppw;  // problems per 64-lane wave (1..32)
 };
 
 struct MultiArgs {

@@ -52,6 +52,8 @@ class Params(C.Structure):
         ("max_iters", C.c_int32),
         ("variant", C.c_int32),
         ("lambda_", C.c_double),
+        ("problems_per_wave", C.c_int32),
+        ("reserved", C.c_int32),
     ]
 
 

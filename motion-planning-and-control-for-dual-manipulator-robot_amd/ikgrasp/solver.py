@@ -74,8 +74,9 @@ class IKSolver:
     def nq(self) -> int:
         return self.model.nq
 
-    def params(self, eps=1e-3, dt=1e-2, max_iters=1000, lam=0.0, variant=_lib.IKG_VARIANT_AUTO):
-        return _lib.default_params(eps=eps, dt=dt, max_iters=max_iters, lambda_=lam, variant=variant)
+    def params(self, eps=1e-3, dt=1e-2, max_iters=1000, lam=0.0, variant=_lib.IKG_VARIANT_AUTO, ppw=0):
+        return _lib.default_params(eps=eps, dt=dt, max_iters=max_iters, lambda_=lam, variant=variant,
+                                   problems_per_wave=ppw)
 
     # ------------------------------------------------------------------ batch
     def solve(self, targets, q0, dtype="f64", stream=None, **kw) -> Solution:

@@ -221,3 +221,12 @@ def test_multistart_selects_best_seed(solver):
         k = t * S + best[t]
         assert np.array_equal(ms.q[t], full.q[k])
         assert ms.converged[t] == full.converged[k] and ms.iters[t] == full.iters[k]
+
+
+def test_problems_per_wave_does_not_change_results(solver):
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(300, seed=9)
+    ref = solver.solve(tg, np.zeros(15), ppw=32)
+    for ppw in (1, 3, 4, 16):
+        s = solver.solve(tg, np.zeros(15), ppw=ppw)
+        assert np.array_equal(s.q, ref.q) and np.array_equal(s.iters, ref.iters) and np.array_equal(s.err, ref.err)
