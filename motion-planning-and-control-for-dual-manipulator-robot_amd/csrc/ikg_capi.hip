@@ -209,7 +209,8 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   int rc = model->device_tables<T>(device, &dm);
   if (rc) return rc;
   const int nq = model->desc.nq;
-  ikg::MultiArgs a{targets, T_, seeds, S, q_out, converged, iters, err_out, best_seed};
+  ikg::MultiArgs a{targets, T_, seeds, S, q_out, converged, iters, err_out, best_seed, nq,
+                   nullptr, nullptr, nullptr, nullptr};
   Staging st(s);
   const bool host = flags & IKG_FLAG_HOST_POINTERS;
   if (host) {
@@ -222,8 +223,20 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
     a.best_seed = best_seed ? (int32_t*)st.out(sizeof(int32_t) * T_) : nullptr;
     if (st.rc) return st.rc;
   }
-  hipError_t e = ikg::launch_multistart<T>(dm, kparams<T>(params), a, model->spec, s);
+  // per-seed workspace, stream-ordered (capturable) allocation
+  const int64_t n = T_ * S;
+  const size_t b_q = sizeof(T) * nq * n, b_err = sizeof(T) * 2 * n, b_it = sizeof(int32_t) * n;
+  char* ws = nullptr;
+  hipError_t e = hipMallocAsync((void**)&ws, b_q + b_err + b_it + n + 64, s);
+  if (e != hipSuccess) return fail(IKG_ENOMEM, "hipMallocAsync(multistart workspace): %s", hipGetErrorString(e));
+  a.ws_q = ws;
+  a.ws_err = ws + b_q;
+  a.ws_iters = (int32_t*)(ws + b_q + b_err);
+  a.ws_conv = (uint8_t*)(ws + b_q + b_err + b_it);
+  e = ikg::launch_multistart<T>(dm, kparams<T>(params), a, model->spec, s);
+  hipError_t e2 = hipFreeAsync(ws, s);
   if (e != hipSuccess) return hip_fail(e, "ikg multistart kernel launch");
+  if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync(multistart workspace)");
   if (host) {
     st.back(q_out, a.q_out, sizeof(T) * nq * T_);
     st.back(converged, a.converged, T_);
@@ -430,7 +443,7 @@ int ikg_solve_multistart(const ikg_model* model, int device, int dtype, const vo
   g_err[0] = 0;
   if (!model) return fail(IKG_EINVAL, "model is NULL");
   if (T < 0 || S <= 0) return fail(IKG_EINVAL, "need T >= 0 and S >= 1");
-  if (S > ikg::kMaxSeedsPerBlock) return fail(IKG_EINVAL, "S=%lld seeds > %d per target", (long long)S, ikg::kMaxSeedsPerBlock);
+  if (S > (int64_t)1 << 24) return fail(IKG_EINVAL, "S=%lld seeds per target is too many", (long long)S);
   if (T > 0 && (!targets || !seeds || !q_out)) return fail(IKG_EINVAL, "targets, seeds and q_out are required");
   if (int rc = check_params(params)) return rc;
   if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);

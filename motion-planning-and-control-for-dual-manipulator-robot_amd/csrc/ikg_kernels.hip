@@ -125,7 +125,7 @@ template <typename T, bool DAMPED, class SP>
 __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                                                             const T* __restrict__ targets,
                                                             const T* __restrict__ q0, int64_t q0_stride, int64_t B,
-                                                            int ppw, T* __restrict__ q_out,
+                                                            int64_t S, int ppw, T* __restrict__ q_out,
                                                             uint8_t* __restrict__ conv_out,
                                                             int32_t* __restrict__ iters_out,
                                                             T* __restrict__ err_out) {
@@ -133,9 +133,12 @@ __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __r
   const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
   const int arm = lane & 1;
   if (lane >= 2 * ppw || p >= B) return;  // both lanes of a pair leave together
+  // multi-start (S > 1): problem p = (target p / S, seed p % S)
+  const int64_t tgt = S > 1 ? p / S : p;
+  const int64_t row = S > 1 ? p - tgt * S : p;
   T RT[9], tT[3];
-  hook_target(m, arm, targets + p * 12, RT, tT);
-  const T* qrow = q0 + p * q0_stride;
+  hook_target(m, arm, targets + tgt * 12, RT, tT);
+  const T* qrow = q0 + row * q0_stride;
   T qc, qa[kArmDof];
   load_q(m, arm, qrow, qc, qa);
   int it;
@@ -150,68 +153,52 @@ __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __r
   if (err_out) err_out[p * 2 + arm] = nrm;
 }
 
-// Multi-start: one workgroup per target, seed i on lanes (2i, 2i+1); the
-// best seed is reduced in LDS inside the workgroup (no cross-GPU traffic).
-template <typename T, bool DAMPED, class SP>
-__global__ __launch_bounds__(1024) void ikg_multistart_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
-                                                              const T* __restrict__ targets,
-                                                              const T* __restrict__ seeds, int64_t S,
-                                                              T* __restrict__ q_out, uint8_t* __restrict__ conv_out,
-                                                              int32_t* __restrict__ iters_out,
-                                                              T* __restrict__ err_out,
-                                                              int32_t* __restrict__ best_out) {
-  __shared__ T s_key[kMaxSeedsPerBlock];
-  __shared__ int s_idx[kMaxSeedsPerBlock];
-  const int64_t tgt = blockIdx.x;
-  const int seed = threadIdx.x >> 1;
-  const int arm = threadIdx.x & 1;
-  const bool active = seed < S;
-  int n = 1;  // power-of-two reduction width covering every seed slot
-  while (n < (int)(blockDim.x >> 1)) n <<= 1;
-  if ((int)threadIdx.x < n) {
-    s_key[threadIdx.x] = T(3.0e38);
-    s_idx[threadIdx.x] = threadIdx.x;
-  }
-  T qc = T(0), qa[kArmDof] = {};
-  int it = 0;
-  bool conv = false;
-  T nrm = T(0), other = T(0);
-  const T* qrow = seeds + (int64_t)(active ? seed : 0) * m->nq;
-  if (active) {
-    T RT[9], tT[3];
-    hook_target(m, arm, targets + tgt * 12, RT, tT);
-    load_q(m, arm, qrow, qc, qa);
-    solve_pair<T, DAMPED, SP>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
-  }
-  __syncthreads();
-  // key: converged seeds rank by the worse hand error; unconverged ones after
-  // them (offset 1e30); ties resolve to the lower seed index.
-  if (arm == 0 && active) {
-    const T worst = fmax(nrm, other);
-    s_key[seed] = conv ? worst : T(1e30) + worst;
-  }
-  __syncthreads();
-  for (int stride = n / 2; stride > 0; stride >>= 1) {
-    const int i = threadIdx.x;
-    if (i < stride) {
-      const T ka = s_key[i], kb = s_key[i + stride];
-      const int ia = s_idx[i], ib = s_idx[i + stride];
-      if (kb < ka || (kb == ka && ib < ia)) {
-        s_key[i] = kb;
-        s_idx[i] = ib;
-      }
+// Multi-start best-seed reduction: one wave per target reduces the S seed
+// results the pair kernel wrote for it (key = worse hand error, converged
+// seeds first, ties to the lower seed index) with DPP/permute wave reductions,
+// then copies the winner's outputs.
+template <typename T>
+__global__ __launch_bounds__(256) void ikg_best_seed_kernel(int64_t T_, int64_t S, int nq,
+                                                            const T* __restrict__ q_all,
+                                                            const uint8_t* __restrict__ conv_all,
+                                                            const int32_t* __restrict__ iters_all,
+                                                            const T* __restrict__ err_all, T* __restrict__ q_out,
+                                                            uint8_t* __restrict__ conv_out,
+                                                            int32_t* __restrict__ iters_out,
+                                                            T* __restrict__ err_out, int32_t* __restrict__ best_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t tgt = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (tgt >= T_) return;  // whole waves leave together
+  T best_key = T(3.0e38);
+  int best = 0x7fffffff;
+  for (int64_t sd = lane; sd < S; sd += 64) {
+    const int64_t k = tgt * S + sd;
+    const T worst = fmax(err_all[2 * k], err_all[2 * k + 1]);
+    const T key = conv_all[k] ? worst : T(1e30) + worst;
+    if (key < best_key) {  // seeds visited in increasing order per lane
+      best_key = key;
+      best = (int)sd;
     }
-    __syncthreads();
   }
-  const int best = s_idx[0];
-  if (active && seed == best) {
-    store_q(m, arm, qrow, it, qc, qa, q_out + tgt * m->nq);
-    if (arm == 0) {
-      if (conv_out) conv_out[tgt] = conv ? 1 : 0;
-      if (iters_out) iters_out[tgt] = it;
-      if (best_out) best_out[tgt] = best;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const T ok = __shfl_xor(best_key, off);
+    const int oi = __shfl_xor(best, off);
+    if (ok < best_key || (ok == best_key && oi < best)) {
+      best_key = ok;
+      best = oi;
     }
-    if (err_out) err_out[tgt * 2 + arm] = nrm;
+  }
+  const int64_t k = tgt * S + best;
+  for (int j = lane; j < nq; j += 64) q_out[tgt * nq + j] = q_all[k * nq + j];
+  if (lane == 0) {
+    if (conv_out) conv_out[tgt] = conv_all[k];
+    if (iters_out) iters_out[tgt] = iters_all[k];
+    if (err_out) {
+      err_out[2 * tgt] = err_all[2 * k];
+      err_out[2 * tgt + 1] = err_all[2 * k + 1];
+    }
+    if (best_out) best_out[tgt] = best;
   }
 }
 
@@ -283,7 +270,7 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
   const int ppw = a.ppw;
   const dim3 grid((unsigned)((a.B + ppw - 1) / ppw));
   hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP>), grid, dim3(64), 0, s, dmodel, prm,
-                     (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, ppw, (T*)a.q_out, a.converged,
+                     (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out, a.converged,
                      a.iters, (T*)a.err_out);
 }
 
@@ -306,31 +293,20 @@ hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, con
   return hipGetLastError();
 }
 
-template <typename T, bool DAMPED, class SP>
-static void launch_multistart_t(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, hipStream_t s) {
-  const int block = (int)(((a.S * 2) + 63) / 64 * 64);
-  const dim3 grid((unsigned)a.T);
-  hipLaunchKernelGGL((ikg_multistart_kernel<T, DAMPED, SP>), grid, dim3(block), 0, s, dmodel, prm,
-                     (const T*)a.targets, (const T*)a.seeds, a.S, (T*)a.q_out, a.converged, a.iters,
-                     (T*)a.err_out, a.best_seed);
-}
-
 template <typename T>
 hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, int spec,
                              hipStream_t s) {
   if (a.T <= 0) return hipSuccess;
-  const bool damped = prm.lambda > T(0);
-  if (spec == kSpecNextage) {
-    if (damped)
-      launch_multistart_t<T, true, SpecNextage>(dmodel, prm, a, s);
-    else
-      launch_multistart_t<T, false, SpecNextage>(dmodel, prm, a, s);
-  } else {
-    if (damped)
-      launch_multistart_t<T, true, SpecGeneric>(dmodel, prm, a, s);
-    else
-      launch_multistart_t<T, false, SpecGeneric>(dmodel, prm, a, s);
-  }
+  // 1) every (target, seed) problem through the pair kernel into the workspace
+  BatchArgs b{a.targets, a.seeds, a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
+  hipError_t e = launch_pair_batch<T>(dmodel, prm, b, spec, s);
+  if (e != hipSuccess) return e;
+  // 2) one wave per target picks the best seed
+  const int block = 256;
+  const dim3 grid((unsigned)((a.T * 64 + block - 1) / block));
+  hipLaunchKernelGGL((ikg_best_seed_kernel<T>), grid, dim3(block), 0, s, a.T, a.S, a.nq, (const T*)a.ws_q,
+                     (const uint8_t*)a.ws_conv, (const int32_t*)a.ws_iters, (const T*)a.ws_err, (T*)a.q_out,
+                     a.converged, a.iters, (T*)a.err_out, a.best_seed);
   return hipGetLastError();
 }
 

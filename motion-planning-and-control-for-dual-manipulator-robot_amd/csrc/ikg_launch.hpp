@@ -17,7 +17,8 @@ struct BatchArgs {
   uint8_t* converged;
   int32_t* iters;
   void* err_out;
-  int ppw;  // problems per 64-lane wave (1..32)
+  int ppw;         // problems per 64-lane wave (1..32)
+  int64_t S = 1;   // seeds per target (multi-start): problem p = (target p / S, q0 row p % S)
 };
 
 struct MultiArgs {
@@ -30,6 +31,12 @@ struct MultiArgs {
   int32_t* iters;
   void* err_out;
   int32_t* best_seed;
+  int nq;
+  // workspace for the S x T per-seed results (device, caller-owned)
+  void* ws_q;
+  uint8_t* ws_conv;
+  int32_t* ws_iters;
+  void* ws_err;
 };
 
 // kernel specialisation chosen at model creation (ikg_model_build.hpp)
@@ -54,6 +61,6 @@ template <typename T>
 hipError_t launch_pair_state(const KModel<T>* dm, const void* targets, const void* q0, int64_t stride, int64_t B,
                              void* out, hipStream_t s);
 
-constexpr int kMaxSeedsPerBlock = 512;
+
 
 }  // namespace ikg

@@ -75,8 +75,8 @@ def test_solve_rejects_bad_arguments_before_touching_the_device():
     p = _lib.default_params()
     rc = lib.ikg_solve_batch(h, 0, 5, buf, buf, 0, 1, C.byref(p), buf, None, None, None, None, 0)
     assert rc == -1 and "dtype" in lib.ikg_last_error().decode()
-    rc = lib.ikg_solve_multistart(h, 0, 0, buf, 1, buf, 1000, C.byref(p), buf, None, None, None, None, None, 0)
-    assert rc == -1 and "seeds" in lib.ikg_last_error().decode()
+    rc = lib.ikg_solve_multistart(h, 0, 0, buf, 1, buf, 0, C.byref(p), buf, None, None, None, None, None, 0)
+    assert rc == -1 and "S >= 1" in lib.ikg_last_error().decode()
     lib.ikg_model_destroy(h)
 
 
