@@ -72,6 +72,9 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--multistart", type=int, default=0,
+                    help="seeds per target (BASELINE configs[4]): every target solved from S random seeds, "
+                         "best seed kept; value counts converged targets/s")
     args = ap.parse_args()
 
     import torch
@@ -87,7 +90,7 @@ def main():
 
     from ikgrasp import _lib
     from ikgrasp.solver import IKSolver
-    from ikgrasp.workload import uniform_targets
+    from ikgrasp.workload import random_seeds, uniform_targets
 
     solver = IKSolver(device=local)
     B = args.batch
@@ -103,11 +106,20 @@ def main():
     gathered = [torch.empty_like(q_out) for _ in range(world)] if (world > 1 and rank == 0) else None
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
+    S = args.multistart
+    if S:
+        seeds_np = random_seeds(solver.model, S, seed=1000 + rank)
+        seeds_np[0] = 0.0  # robot.q0 is always one of the seeds
+        seeds = torch.tensor(seeds_np, dtype=tdt, device=dev)
+        best = torch.empty(B, dtype=torch.int32, device=dev)
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        solver.solve_into(targets, q0, q_out, conv, iters, err, code, sh, variant=args.variant)
+        if S:
+            solver.solve_multistart_into(targets, seeds, q_out, conv, iters, err, best, code, sh)
+        else:
+            solver.solve_into(targets, q0, q_out, conv, iters, err, code, sh, variant=args.variant)
         if ev is not None:
             ev[1].record(stream)
         if world > 1 and not args.no_gather:
@@ -144,7 +156,9 @@ def main():
     if rank == 0:
         per_step = elapsed / args.steps
         value = tot_conv / per_step
-        flops = (sum_iters * F_ITER) / (kern_ms * 1e-3) / 1e12  # rank-0 kernel, TFLOP/s
+        if S:  # iterations of every (target, seed) problem: not returned per seed; use the launch count
+            sum_iters = None
+        flops = (sum_iters * F_ITER) / (kern_ms * 1e-3) / 1e12 if sum_iters else None  # rank-0 kernel, TFLOP/s
         abytes = algorithmic_bytes(args.dtype, B)
         traffic = None
         pmc = os.path.join(ROOT, "profiles", f"pmc_{args.dtype}_b{B}.json")
@@ -157,8 +171,11 @@ def main():
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (cube targets ~ path.py:35-47 sampler, seed = rank; q0 = robot.q0 = 0)",
             "config": {
-                "workload": (f"BASELINE configs[1]: batch {B} grasp targets per GPU, {args.dtype}, "
+                "workload": (f"BASELINE configs[4]: multi-start {S} seeds x {B} targets per GPU, {args.dtype}"
+                             if S else
+                             f"BASELINE configs[1]: batch {B} grasp targets per GPU, {args.dtype}, "
                              f"pair kernel (2 lanes/problem)"),
+                "seeds_per_target": S or 1,
                 "batch_per_gpu": B, "global_batch": B * world, "yaw_range": args.yaw,
                 "parallelism": f"shard{world}" + ("" if world == 1 or args.no_gather else "+rccl_gather_q"),
             },
@@ -167,7 +184,7 @@ def main():
             "mean_iters": tot_iters / tot_B,
             "roofline": {
                 "bound": "valu", "achieved": flops, "peak": PEAK_VALU[args.dtype], "unit": "TFLOP/s",
-                "frac": flops / PEAK_VALU[args.dtype], "traffic": traffic,
+                "frac": flops / PEAK_VALU[args.dtype] if flops else None, "traffic": traffic,
                 "kernel": "ikg_pair_batch_kernel", "kernel_ms": kern_ms,
                 "work": f"sum(iters)={sum_iters} x {F_ITER} FP ops (SURVEY §8a)",
             },
@@ -177,7 +194,7 @@ def main():
                 "algorithmic_bytes": abytes,
             },
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not S:
             out["cpu_baseline"] = cpu_baseline(tg_np)
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -132,6 +132,14 @@ class IKSolver:
             targets.shape[0], C.byref(prm), q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(),
             err.data_ptr(), C.c_void_p(stream_handle), 0))
 
+    def solve_multistart_into(self, targets, seeds, q_out, conv, iters, err, best, dtype_code, stream_handle, **kw):
+        """Raw device-pointer multi-start launch (preallocated torch tensors; bench.py)."""
+        prm = self.params(**kw)
+        _lib.check(self.lib.ikg_solve_multistart(
+            self._h, targets.device.index or 0, dtype_code, targets.data_ptr(), targets.shape[0], seeds.data_ptr(),
+            seeds.shape[0], C.byref(prm), q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(), err.data_ptr(),
+            best.data_ptr(), C.c_void_p(stream_handle), 0))
+
     # ------------------------------------------------------------------ multistart
     def solve_multistart(self, targets, seeds, dtype="f64", **kw) -> Solution:
         """S seeds x T targets -> best seed per target (ikg_solve_multistart)."""
