@@ -110,6 +110,30 @@ struct Prec<float> {
 template <typename T>
 IKG_HD inline T sel(bool b, T x, T y) { return b ? x : y; }
 
+// a / b through the hardware reciprocal refined by Newton steps (fp64: 2 steps
+// + one residual correction, within ~1 ulp of the IEEE quotient) instead of the
+// 11-instruction div_scale/div_fmas/div_fixup sequence; none of the quotients
+// on the IK path needs correct rounding.
+template <typename T>
+IKG_HD inline T fdiv(T a, T b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  if constexpr (sizeof(T) == 8) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(r, fma(-b, r, 1.0), r);
+    r = fma(r, fma(-b, r, 1.0), r);
+    const double q = a * r;
+    return fma(fma(-b, q, a), r, q);
+  } else {
+    float r = __builtin_amdgcn_rcpf(b);
+    r = fmaf(r, fmaf(-b, r, 1.0f), r);
+    const float q = a * r;
+    return fmaf(fmaf(-b, q, a), r, q);
+  }
+#else
+  return a / b;
+#endif
+}
+
 // ---------------------------------------------------------------- cross-lane
 // Exchange a value with the partner lane (lane ^ 1) through a DPP quad_perm
 // [1,0,3,2]: no LDS traffic, one VALU op per dword.
@@ -226,11 +250,11 @@ IKG_HD inline void log6(const T* R, const T* p, T* e) {
     w[1] = (R[2] > R[6] ? T(1) : T(-1)) * (t1 > T(0) ? sqrt(t1) : T(0));
     w[2] = (R[3] > R[1] ? T(1) : T(-1)) * (tt > T(0) ? sqrt(tt) : T(0));
     // here sin(theta) from |skew| is inaccurate; 1 - cos(theta) ~ 2 is benign
-    alpha = theta * (-s_) / (T(2) * (T(1) - ct));  // sin(theta) = -sin(theta - pi)
+    alpha = fdiv(theta * (-s_), T(2) * (T(1) - ct));  // sin(theta) = -sin(theta - pi)
   } else {
     T f;
     if (theta > Prec<T>::kPrec3) {
-      f = theta / st;
+      f = fdiv(theta, st);
     } else if constexpr (sizeof(T) == 8) {
       f = T(1);  // Pinocchio: theta/sin(theta) -> 1 below precision<3>()
     } else {
@@ -241,7 +265,10 @@ IKG_HD inline void log6(const T* R, const T* p, T* e) {
     w[1] = hf * sy;
     w[2] = hf * sz;
     // theta (1+cos)/(2 sin) for cos >= 0, theta sin/(2(1-cos)) otherwise: no cancellation
-    alpha = ct >= T(0) ? hf * (T(1) + ct) : theta * st / (T(2) * (T(1) - ct));
+    if (ct >= T(0))
+      alpha = hf * (T(1) + ct);
+    else
+      alpha = fdiv(theta * st, T(2) * (T(1) - ct));
   }
   T beta;
   if (theta < Prec<T>::kPrec3) {
@@ -253,7 +280,7 @@ IKG_HD inline void log6(const T* R, const T* p, T* e) {
       beta = T(1) / T(12) + t2 * (T(1) / T(720) + t2 * (T(1) / T(30240) + t2 * (T(1) / T(1209600))));
     }
   } else {
-    beta = (T(1) - alpha) / t2;
+    beta = fdiv(T(1) - alpha, t2);
   }
   const T wp = w[0] * p[0] + w[1] * p[1] + w[2] * p[2];
   const T bwp = beta * wp;
@@ -606,8 +633,8 @@ IKG_HD inline void cross3(const T* a, const T* b, T* c) {
 template <typename T>
 IKG_HD inline T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
 
-// [g1 g2 g3]^-1 applied to b0 and b1 by the adjugate (Cramer); a determinant
-// below rcond * |g1||g2||g3| truncates the inverse to zero (pinv's rcond).
+// [g1 g2 g3]^-1 applied to b0 and b1 by the adjugate (Cramer); an exactly
+// singular block gives a zero inverse (pinv truncates only below 1e-15 sigma_max).
 template <typename T>
 IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b0, const T* b1, T* x0, T* x1) {
   T r1[3], r2[3], r3[3];
@@ -615,9 +642,7 @@ IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b
   cross3(g3, g1, r2);
   cross3(g1, g2, r3);
   const T det = dot3(g1, r1);
-  const T bound = dot3(g1, g1) * dot3(g2, g2) * dot3(g3, g3);
-  const T rc = Prec<T>::kRcond;
-  const T rdet = det * det > rc * rc * bound ? T(1) / det : T(0);
+  const T rdet = det != T(0) ? fdiv(T(1), det) : T(0);
   x0[0] = dot3(r1, b0) * rdet;
   x0[1] = dot3(r2, b0) * rdet;
   x0[2] = dot3(r3, b0) * rdet;
@@ -719,7 +744,7 @@ IKG_HD inline void arm_solve_damped(const T (&A)[6][8], T lambda, T* ze, T* zc, 
 // Sherman–Morrison chest step from the pair-summed scalars.
 template <typename T>
 IKG_HD inline T chest_step(T alpha_sum, T beta_sum) {
-  return alpha_sum / (T(1) + beta_sum);
+  return fdiv(alpha_sum, T(1) + beta_sum);
 }
 
 template <typename T>

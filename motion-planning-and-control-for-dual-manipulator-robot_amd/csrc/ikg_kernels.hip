@@ -19,6 +19,8 @@
 // No LDS, no barriers; the model tables are read with uniform scalar loads.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "ikg_device.hpp"
 #include "ikg_launch.hpp"
 
@@ -122,7 +124,7 @@ __device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T
 // A wave's issue cost does not depend on how many lanes are active, so small
 // batches are spread with ppw < 32 to occupy every SIMD.
 template <typename T, bool DAMPED, class SP>
-__global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
+__global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             const T* __restrict__ targets,
                                                             const T* __restrict__ q0, int64_t q0_stride, int64_t B,
                                                             int64_t S, int ppw, T* __restrict__ q_out,
@@ -130,6 +132,10 @@ __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __r
                                                             int32_t* __restrict__ iters_out,
                                                             T* __restrict__ err_out) {
   const int lane = threadIdx.x;
+  // model tables stay in global memory: the compiler hoists them into
+  // registers (staging them in LDS and re-reading per iteration measured 8%
+  // slower)
+  const KModel<T>* m = gm;
   const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
   const int arm = lane & 1;
   if (lane >= 2 * ppw || p >= B) return;  // both lanes of a pair leave together
@@ -265,11 +271,23 @@ __global__ __launch_bounds__(256) void ikg_log6_kernel(const T* __restrict__ M, 
 }
 
 // ------------------------------------------------------------------ launchers
+// Experiment knob (tools/spread_sweep.py): dynamic LDS reserved per
+// single-wave workgroup, which caps how many workgroups the dispatcher packs
+// onto one CU.
+static size_t lds_pad_bytes() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("IKG_LDS_PAD");
+    v = e ? atol(e) : 0;
+  }
+  return (size_t)v;
+}
+
 template <typename T, bool DAMPED, class SP>
 static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
   const int ppw = a.ppw;
   const dim3 grid((unsigned)((a.B + ppw - 1) / ppw));
-  hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP>), grid, dim3(64), 0, s, dmodel, prm,
+  hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP>), grid, dim3(64), lds_pad_bytes(), s, dmodel, prm,
                      (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out, a.converged,
                      a.iters, (T*)a.err_out);
 }

@@ -1,0 +1,28 @@
+"""Run one IK configuration `reps` times (for rocprofv3 --pmc passes).
+usage: pmc_probe.py B dtype ppw reps"""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd"))
+from ikgrasp.solver import IKSolver  # noqa: E402
+from ikgrasp.workload import uniform_targets  # noqa: E402
+
+B, dtype, ppw, reps = int(sys.argv[1]), sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+s = IKSolver()
+dev = torch.device("cuda", 0)
+tdt = torch.float64 if dtype == "f64" else torch.float32
+code = 0 if dtype == "f64" else 1
+tg = torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device=dev)
+q0 = torch.zeros(15, dtype=tdt, device=dev)
+qo = torch.empty((B, 15), dtype=tdt, device=dev)
+cv = torch.empty(B, dtype=torch.uint8, device=dev)
+it = torch.empty(B, dtype=torch.int32, device=dev)
+er = torch.empty((B, 2), dtype=tdt, device=dev)
+st = torch.cuda.current_stream().cuda_stream
+for _ in range(reps):
+    s.solve_into(tg, q0, qo, cv, it, er, code, st, ppw=ppw)
+torch.cuda.synchronize()
+print("sum iters", int(it.to(torch.int64).sum()), "converged", int(cv.sum()))
