@@ -69,9 +69,9 @@ __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams
     trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }
   it_out = it;
-  conv_out = conv;
   nrm_out = nrm;
   other_out = other;
+  conv_out = conv;
 }
 
 // tools.getcubeplacement: oMcube * hook (tools.py:54-59), for this lane's arm.
