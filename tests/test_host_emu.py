@@ -1,0 +1,80 @@
+"""Kernel arithmetic on the CPU through the host emulator (ikg_host_emu.hip:
+the exact stage functions of ikg_device.hpp composed for both arm lanes).
+This is test tooling, not the product path; it lets the CPU suite cover the
+specialised (spherical-wrist, compile-time axes) and generic (runtime axes,
+Householder QR) solves against the oracle fixtures without a GPU."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from ikgrasp import _lib
+from ikgrasp.model import load_nextage
+
+EMU = os.path.join(os.path.dirname(_lib.LIB_PATH), "libikgrasp_emu.so")
+GENERIC = 99  # ikg_params.variant value the emulator reads as "force the generic path"
+
+
+@pytest.fixture(scope="module")
+def emu():
+    if not os.path.exists(EMU):
+        pytest.skip("libikgrasp_emu.so not built")
+    lib = C.CDLL(EMU)
+    vp = C.c_void_p
+    lib.ikg_emu_solve.argtypes = [vp, C.c_int, vp, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, vp, C.c_int]
+    desc = _lib.model_desc(load_nextage())
+
+    def solve(targets, q0, dtype=0, **kw):
+        npt = np.float64 if dtype == 0 else np.float32
+        tg = np.ascontiguousarray(targets, dtype=npt).reshape(-1, 12)
+        B = len(tg)
+        q0 = np.ascontiguousarray(np.broadcast_to(q0, (B, 15)), dtype=npt)
+        p = _lib.default_params(**kw)
+        q = np.empty((B, 15), npt)
+        conv = np.empty(B, np.uint8)
+        it = np.empty(B, np.int32)
+        err = np.empty((B, 2), npt)
+        lib.ikg_emu_solve(C.byref(desc), dtype, tg.ctypes.data, q0.ctypes.data, 15, B, C.byref(p), q.ctypes.data,
+                          conv.ctypes.data, it.ctypes.data, err.ctypes.data, None, 0)
+        return q, conv.astype(bool), it, err
+
+    return solve
+
+
+def _kat_targets(kat):
+    rows = []
+    for k in ("cube_placement", "cube_placement_target"):
+        rows.append(np.concatenate([np.array(kat[k]["R"]).reshape(9), kat[k]["t"]]))
+    return np.array(rows)
+
+
+@pytest.mark.parametrize("variant", [0, GENERIC])
+def test_emulated_kernel_kats(emu, kat, variant):
+    q, conv, it, err = emu(_kat_targets(kat), np.zeros(15), variant=variant)
+    assert conv.all() and it.tolist() == [740, 736]
+    assert np.abs(q[0] - kat["q0"]).max() <= 1e-12
+    assert np.abs(q[1] - kat["qe"]).max() <= 1e-12
+
+
+@pytest.mark.parametrize("variant", [0, GENERIC])
+def test_emulated_kernel_fixtures_fp64(emu, oracle_cases, variant):
+    c = oracle_cases
+    q, conv, it, err = emu(c["targets"], c["q0"], variant=variant)
+    assert np.array_equal(conv, c["converged"]) and np.array_equal(it, c["iters"])
+    ok = c["converged"]
+    assert np.abs(q[ok] - c["q"][ok]).max() <= 1e-9
+
+
+def test_emulated_kernel_fp32_kat(emu, kat):
+    q, conv, it, err = emu(_kat_targets(kat), np.zeros(15), dtype=1)
+    assert conv.all() and (np.abs(it - np.array([740, 736])) <= 2).all()
+    assert np.abs(q[0] - kat["q0"]).max() <= 1e-5
+
+
+def test_emulated_damped_variant_matches_damped_oracle(emu, kat):
+    from oracle import ik_oracle as o
+    tg = _kat_targets(kat)[:1]
+    q, conv, it, err = emu(tg, np.zeros(15), lambda_=1e-4, max_iters=150)
+    qo, ok, ito, _ = o.computeqgrasppose(np.zeros(15), np.eye(3), tg[0, 9:], lam=1e-4, max_iters=150)
+    assert it[0] == ito and np.abs(q[0] - qo).max() <= 1e-9
