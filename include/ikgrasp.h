@@ -37,6 +37,8 @@ extern "C" {
 
 #define IKG_MAX_NQ 32
 #define IKG_ARM_DOF 6
+#define IKG_MAX_GEOMS 64
+#define IKG_MAX_PAIRS 1024
 
 enum ikg_dtype { IKG_F64 = 0, IKG_F32 = 1 };
 
@@ -82,14 +84,38 @@ typedef struct ikg_params {
   int32_t variant;     /* enum ikg_variant */
   double lambda;       /* damping of (J J^T + lambda I); 0 = pinv semantics (reference) */
   int32_t problems_per_wave; /* 1..32 problems per 64-lane wave; 0 = auto (32) */
-  int32_t reserved;
+  int32_t check_collision;   /* 1: reference `success` = converged AND collision-free, iterating on while
+                                converged-but-colliding (inverse_geometry.py:70, :97-98); needs
+                                ikg_model_set_collision.  0: convergence only (default). */
 } ikg_params;
+
+/* Collision scene (tools.py:25-35 collision(); pairs built in
+ * setup_pinocchio.py:53-60), produced by ikgrasp/collision.py. */
+enum ikg_geom_kind {
+  IKG_GEOM_SPHERE = 0,    /* dims: radius */
+  IKG_GEOM_BOX = 1,       /* dims: half extents */
+  IKG_GEOM_CYLINDER = 2,  /* dims: radius, half length (local z) */
+  IKG_GEOM_MESHBOX = 3    /* convex hull of a box mesh (the cube): half extents */
+};
+typedef struct ikg_collision_desc {
+  int32_t n_geoms;
+  int32_t kind[IKG_MAX_GEOMS];
+  int32_t joint[IKG_MAX_GEOMS];          /* q index of the parent joint, -1 = world-fixed */
+  double placement[IKG_MAX_GEOMS][12];   /* in the parent joint frame (world if joint = -1) */
+  double dims[IKG_MAX_GEOMS][3];
+  int32_t target_geom;                   /* geometry placed at each solve's cube target, -1 none */
+  int32_t n_pairs;
+  int32_t pairs[IKG_MAX_PAIRS][2];
+} ikg_collision_desc;
 
 typedef struct ikg_model ikg_model;
 
 /* Build a device-ready model (tables are uploaded to every device lazily). */
 int ikg_model_create(const ikg_model_desc* desc, ikg_model** out);
 void ikg_model_destroy(ikg_model* model);
+
+/* Attach (or replace) the collision scene of a model. */
+int ikg_model_set_collision(ikg_model* model, const ikg_collision_desc* desc);
 
 /* Fill `p` with the reference defaults. */
 void ikg_params_default(ikg_params* p);
@@ -138,6 +164,14 @@ int ikg_fk_batch(const ikg_model* model, int device, int dtype,
  * inverse_geometry.py:66-67): M [B,12] -> out [B,6] = [v; w].
  */
 int ikg_log6_batch(int device, int dtype, const void* M, int64_t B, void* out, void* stream, uint32_t flags);
+
+/*
+ * Batched collision query, tools.collision(robot, q) (tools.py:25-35) with the
+ * cube placed at each target (setcubeplacement, tools.py:62-68):
+ *   q [B,nq], targets [B,12] -> in_collision [B] (1 = some active pair intersects)
+ */
+int ikg_collision_batch(const ikg_model* model, int device, int dtype, const void* q, const void* targets,
+                        int64_t B, uint8_t* in_collision, void* stream, uint32_t flags);
 
 /* Thread-local message of the last failure ("" if none). */
 const char* ikg_last_error(void);

@@ -44,26 +44,45 @@ struct ikg_model {
   std::mutex mu;
   std::vector<void*> dev64;  // per device
   std::vector<void*> dev32;
+  // collision scene (ikg_model_set_collision)
+  bool has_collision = false;
+  ikg::KCollision<double> c64;
+  ikg::KCollision<float> c32;
+  std::vector<void*> col64;
+  std::vector<void*> col32;
 
-  template <typename T>
-  int device_tables(int device, const ikg::KModel<T>** out) {
+  // Upload `bytes` of `src` to `slot[device]` once; the slot is reused after.
+  int upload(std::vector<void*>& slot, int device, const void* src, size_t bytes, const void** out) {
     std::lock_guard<std::mutex> lock(mu);
-    std::vector<void*>& slot = sizeof(T) == 8 ? dev64 : dev32;
     if ((int)slot.size() <= device) slot.resize(device + 1, nullptr);
     if (!slot[device]) {
       void* p = nullptr;
-      hipError_t e = hipMalloc(&p, sizeof(ikg::KModel<T>));
+      hipError_t e = hipMalloc(&p, bytes);
       if (e != hipSuccess) return fail(IKG_ENOMEM, "hipMalloc(model tables): %s", hipGetErrorString(e));
-      const void* src = sizeof(T) == 8 ? (const void*)&k64 : (const void*)&k32;
-      e = hipMemcpy(p, src, sizeof(ikg::KModel<T>), hipMemcpyHostToDevice);
+      e = hipMemcpy(p, src, bytes, hipMemcpyHostToDevice);
       if (e != hipSuccess) {
         (void)hipFree(p);
         return hip_fail(e, "hipMemcpy(model tables)");
       }
       slot[device] = p;
     }
-    *out = (const ikg::KModel<T>*)slot[device];
+    *out = slot[device];
     return IKG_OK;
+  }
+
+  template <typename T>
+  int device_tables(int device, const ikg::KModel<T>** out) {
+    const bool d = sizeof(T) == 8;
+    return upload(d ? dev64 : dev32, device, d ? (const void*)&k64 : (const void*)&k32, sizeof(ikg::KModel<T>),
+                  (const void**)out);
+  }
+
+  template <typename T>
+  int collision_tables(int device, const ikg::KCollision<T>** out) {
+    if (!has_collision) return fail(IKG_EINVAL, "no collision scene attached (ikg_model_set_collision)");
+    const bool d = sizeof(T) == 8;
+    return upload(d ? col64 : col32, device, d ? (const void*)&c64 : (const void*)&c32, sizeof(ikg::KCollision<T>),
+                  (const void**)out);
   }
 };
 
@@ -137,6 +156,15 @@ struct Staging {
   }
 };
 
+void free_slots(std::vector<void*>& slot) {
+  for (size_t i = 0; i < slot.size(); ++i)
+    if (slot[i]) {
+      (void)hipSetDevice((int)i);
+      (void)hipFree(slot[i]);
+      slot[i] = nullptr;
+    }
+}
+
 // Problems per wave.  Full 32-problem waves are fastest at every batch size
 // measured (B = 4k..131k, fp32/fp64): spreading a small batch over more,
 // sparser waves was 1.3-3x SLOWER (profiles/r01/ppw_sweep.txt).
@@ -152,6 +180,7 @@ int check_params(const ikg_params* p) {
     return fail(IKG_EINVAL, "variant %d not available in this build", p->variant);
   if (p->problems_per_wave < 0 || p->problems_per_wave > 32)
     return fail(IKG_EINVAL, "problems_per_wave must be in [0, 32]");
+  if (p->check_collision != 0 && p->check_collision != 1) return fail(IKG_EINVAL, "check_collision must be 0 or 1");
   return IKG_OK;
 }
 
@@ -172,6 +201,8 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   const ikg::KModel<T>* dm = nullptr;
   int rc = model->device_tables<T>(device, &dm);
   if (rc) return rc;
+  const ikg::KCollision<T>* dc = nullptr;
+  if (params->check_collision && (rc = model->collision_tables<T>(device, &dc))) return rc;
   const int nq = model->desc.nq;
   ikg::BatchArgs a{targets, q0, q0_stride, B, q_out, converged, iters, err_out, 32};
   a.ppw = params->problems_per_wave > 0 ? params->problems_per_wave : auto_ppw(device, B);
@@ -187,8 +218,18 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
     a.err_out = err_out ? st.out(sizeof(T) * 2 * B) : nullptr;
     if (st.rc) return st.rc;
   }
+  if (dc) {  // the continuation reads and rewrites every per-problem output
+    if (!a.converged) a.converged = (uint8_t*)st.out(B);
+    if (!a.iters) a.iters = (int32_t*)st.out(sizeof(int32_t) * B);
+    if (!a.err_out) a.err_out = st.out(sizeof(T) * 2 * B);
+    if (st.rc) return st.rc;
+  }
   hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, model->spec, s);
   if (e != hipSuccess) return hip_fail(e, "ikg pair kernel launch");
+  if (dc) {
+    e = ikg::launch_collide_continue<T>(dm, dc, kparams<T>(params), a, model->spec, s);
+    if (e != hipSuccess) return hip_fail(e, "ikg collision continuation launch");
+  }
   if (host) {
     st.back(q_out, a.q_out, sizeof(T) * nq * B);
     st.back(converged, a.converged, B);
@@ -211,6 +252,11 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   const int nq = model->desc.nq;
   ikg::MultiArgs a{targets, T_, seeds, S, q_out, converged, iters, err_out, best_seed, nq,
                    nullptr, nullptr, nullptr, nullptr};
+  if (params->check_collision) {
+    const ikg::KCollision<T>* dc = nullptr;
+    if ((rc = model->collision_tables<T>(device, &dc))) return rc;
+    a.collision = dc;
+  }
   Staging st(s);
   const bool host = flags & IKG_FLAG_HOST_POINTERS;
   if (host) {
@@ -269,6 +315,36 @@ int fk_t(ikg_model* model, int device, const void* q, int64_t B, void* hands, hi
   if (e != hipSuccess) return hip_fail(e, "ikg fk kernel launch");
   if (host) {
     st.back(hands, dh, sizeof(T) * 24 * B);
+    if (st.rc) return st.rc;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
+  return IKG_OK;
+}
+
+template <typename T>
+int collision_t(ikg_model* model, int device, const void* q, const void* targets, int64_t B, uint8_t* out,
+                hipStream_t s, uint32_t flags) {
+  const ikg::KModel<T>* dm = nullptr;
+  const ikg::KCollision<T>* dc = nullptr;
+  int rc = model->device_tables<T>(device, &dm);
+  if (rc || (rc = model->collision_tables<T>(device, &dc))) return rc;
+  const int nq = model->desc.nq;
+  Staging st(s);
+  const bool host = flags & IKG_FLAG_HOST_POINTERS;
+  const void* dq = q;
+  const void* dt = targets;
+  uint8_t* dout = out;
+  if (host) {
+    dq = st.in(q, sizeof(T) * nq * B);
+    dt = st.in(targets, sizeof(T) * 12 * B);
+    dout = (uint8_t*)st.out(B);
+    if (st.rc) return st.rc;
+  }
+  hipError_t e = ikg::launch_collision<T>(dm, dc, dq, dt, B, dout, s);
+  if (e != hipSuccess) return hip_fail(e, "ikg collision kernel launch");
+  if (host) {
+    st.back(out, dout, B);
     if (st.rc) return st.rc;
     e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
@@ -357,7 +433,7 @@ void ikg_params_default(ikg_params* p) {
   p->variant = IKG_VARIANT_AUTO;
   p->lambda = 0.0;      // np.linalg.pinv semantics
   p->problems_per_wave = 0;
-  p->reserved = 0;
+  p->check_collision = 0;
 }
 
 int ikg_model_create(const ikg_model_desc* d, ikg_model** out) {
@@ -402,16 +478,10 @@ void ikg_model_destroy(ikg_model* m) {
   if (!m) return;
   int prev = -1;
   (void)hipGetDevice(&prev);
-  for (size_t i = 0; i < m->dev64.size(); ++i)
-    if (m->dev64[i]) {
-      (void)hipSetDevice((int)i);
-      (void)hipFree(m->dev64[i]);
-    }
-  for (size_t i = 0; i < m->dev32.size(); ++i)
-    if (m->dev32[i]) {
-      (void)hipSetDevice((int)i);
-      (void)hipFree(m->dev32[i]);
-    }
+  free_slots(m->dev64);
+  free_slots(m->dev32);
+  free_slots(m->col64);
+  free_slots(m->col32);
   if (prev >= 0) (void)hipSetDevice(prev);
   delete m;
 }
@@ -426,6 +496,7 @@ int ikg_solve_batch(const ikg_model* model, int device, int dtype, const void* t
   if (q0_stride != 0 && q0_stride < model->desc.nq) return fail(IKG_EINVAL, "q0_stride must be 0 or >= nq");
   if (int rc = check_params(params)) return rc;
   if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  if (params->check_collision && B > 0x7fffffff) return fail(IKG_EINVAL, "B too large for the collision launch");
   DeviceGuard g(device);
   if (g.rc) return g.rc;
   if (B == 0) return IKG_OK;
@@ -447,6 +518,7 @@ int ikg_solve_multistart(const ikg_model* model, int device, int dtype, const vo
   if (T > 0 && (!targets || !seeds || !q_out)) return fail(IKG_EINVAL, "targets, seeds and q_out are required");
   if (int rc = check_params(params)) return rc;
   if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  if (params->check_collision && T * S > 0x7fffffff) return fail(IKG_EINVAL, "T*S too large for the collision launch");
   DeviceGuard g(device);
   if (g.rc) return g.rc;
   if (T == 0) return IKG_OK;
@@ -472,6 +544,58 @@ int ikg_fk_batch(const ikg_model* model, int device, int dtype, const void* q, i
   hipStream_t s = (hipStream_t)stream;
   return dtype == IKG_F64 ? fk_t<double>(m, device, q, B, hands, s, flags)
                           : fk_t<float>(m, device, q, B, hands, s, flags);
+}
+
+int ikg_model_set_collision(ikg_model* m, const ikg_collision_desc* d) {
+  g_err[0] = 0;
+  if (!m || !d) return fail(IKG_EINVAL, "NULL argument");
+  if (d->n_geoms < 1 || d->n_geoms > IKG_MAX_GEOMS)
+    return fail(IKG_EINVAL, "n_geoms=%d outside [1,%d]", d->n_geoms, IKG_MAX_GEOMS);
+  if (d->n_pairs < 0 || d->n_pairs > IKG_MAX_PAIRS)
+    return fail(IKG_EINVAL, "n_pairs=%d outside [0,%d]", d->n_pairs, IKG_MAX_PAIRS);
+  if (d->target_geom < -1 || d->target_geom >= d->n_geoms) return fail(IKG_EINVAL, "target_geom out of range");
+  for (int g = 0; g < d->n_geoms; ++g) {
+    if (d->kind[g] < IKG_GEOM_SPHERE || d->kind[g] > IKG_GEOM_MESHBOX)
+      return fail(IKG_EINVAL, "geometry %d: unknown kind %d", g, d->kind[g]);
+    if (d->joint[g] < -1 || d->joint[g] >= m->desc.nq)
+      return fail(IKG_EINVAL, "geometry %d: joint %d out of range", g, d->joint[g]);
+    for (int i = 0; i < 3; ++i)
+      if (!(d->dims[g][i] >= 0) || !std::isfinite(d->dims[g][i]))
+        return fail(IKG_EINVAL, "geometry %d: dims must be finite and >= 0", g);
+  }
+  for (int k = 0; k < d->n_pairs; ++k) {
+    const int a = d->pairs[k][0], b = d->pairs[k][1];
+    if (a < 0 || b < 0 || a >= d->n_geoms || b >= d->n_geoms || a == b)
+      return fail(IKG_EINVAL, "pair %d: bad geometry indices (%d, %d)", k, a, b);
+  }
+  std::lock_guard<std::mutex> lock(m->mu);
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  free_slots(m->col64);  // re-uploaded lazily; callers must not race a solve
+  free_slots(m->col32);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  ikg::build_kcollision<double>(*d, m->c64);
+  ikg::build_kcollision<float>(*d, m->c32);
+  m->has_collision = true;
+  return IKG_OK;
+}
+
+int ikg_collision_batch(const ikg_model* model, int device, int dtype, const void* q, const void* targets, int64_t B,
+                        uint8_t* in_collision, void* stream, uint32_t flags) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (B < 0) return fail(IKG_EINVAL, "B must be >= 0");
+  if (B > 0 && (!q || !targets || !in_collision)) return fail(IKG_EINVAL, "q, targets and in_collision are required");
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  if (!model->has_collision) return fail(IKG_EINVAL, "no collision scene attached (ikg_model_set_collision)");
+  if (B > 0x7fffffff) return fail(IKG_EINVAL, "B too large for one launch");
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  if (B == 0) return IKG_OK;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == IKG_F64 ? collision_t<double>(m, device, q, targets, B, in_collision, s, flags)
+                          : collision_t<float>(m, device, q, targets, B, in_collision, s, flags);
 }
 
 }  // extern "C"

@@ -54,6 +54,11 @@ struct KModel {
   T hand_sc[2][2];    // (sin, cos) of that angle per hand
   int32_t wrist;      // 1: axes of arm joints 3,4,5 meet at the origin of arm joint 4
   int32_t pattern;    // compile-time specialisation code (ikg_model_build.hpp)
+  // full kinematic tree (every joint, q order) for the collision check
+  T jR[kMaxNq][9];
+  T jt[kMaxNq][3];
+  int32_t jaxis[kMaxNq];
+  int32_t jparent[kMaxNq];
 };
 
 // ---------------------------------------------------------------- kernel specialisation
@@ -779,4 +784,25 @@ IKG_HD inline void arm_update(const KModel<T>* __restrict__ m, int arm, T dt, T 
     qa[k] = clampq(qa[k] + dq[k] * dt, lo, hi);
   }
 }
+
+// tools.getcubeplacement: oMcube * hook (tools.py:54-59), for this lane's arm.
+template <typename T>
+IKG_HD inline void hook_target(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ tg, T* RT,
+                                   T* tT) {
+  const bool right = arm != 0;
+  T CR[9], Ct[3], HR[9], Ht[3], d[3];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) CR[i] = tg[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) Ct[i] = tg[9 + i];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) HR[i] = sel(right, m->hook_R[1][i], m->hook_R[0][i]);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) Ht[i] = sel(right, m->hook_t[1][i], m->hook_t[0][i]);
+  matmul3(CR, HR, RT);
+  matvec3(CR, Ht, d);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) tT[i] = Ct[i] + d[i];
+}
+
 }  // namespace ikg

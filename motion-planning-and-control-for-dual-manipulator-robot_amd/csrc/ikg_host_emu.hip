@@ -6,15 +6,30 @@
 #include <cstdint>
 #include <cstring>
 
+#include "ikg_collision.hpp"
 #include "ikg_device.hpp"
 #include "ikg_model_build.hpp"
 #include "ikgrasp.h"
 
 namespace {
 
+// collide_wave's stages run serially (same functions, same order per lane).
+template <typename T>
+bool emu_collide(const ikg::KModel<T>& m, const ikg::KCollision<T>& c, const T* q, const T* tgt) {
+  using namespace ikg;
+  T L[kMaxNq][12], F[kMaxNq][12], P[kMaxGeoms][12];
+  for (int j = 0; j < m.nq; ++j) joint_local(&m, j, q[j], L[j]);
+  for (int j = 0; j < m.nq; ++j) joint_world(&m, j, L, F[j]);
+  for (int g = 0; g < c.n_geoms; ++g) geom_world(&c, g, F, tgt, P[g]);
+  for (int k = 0; k < c.n_pairs; ++k)
+    if (pair_hit(&c, k, P)) return true;
+  return false;
+}
+
 template <typename T, class SP>
 void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, const T* tg, const T* qrow,
-             T* qo, uint8_t* conv_out, int32_t* iters_out, T* err_out, T* trace, int trace_len) {
+             T* qo, uint8_t* conv_out, int32_t* iters_out, T* err_out, T* trace, int trace_len,
+             const ikg::KCollision<T>* col) {
   using namespace ikg;
   T RT[2][9], tT[2][3], qc[2], qa[2][kArmDof], sn[2][7], cs[2][7];
   for (int arm = 0; arm < 2; ++arm) {
@@ -42,8 +57,23 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
     }
     if (it >= prm.max_iters) break;
     if (nrm[0] < prm.eps && nrm[1] < prm.eps) {
-      conv = true;
-      break;
+      if (!col) {
+        conv = true;
+        break;
+      }
+      T qn[kMaxNq];  // the current iterate in q order (passive joints clamped after update 1)
+      for (int j = 0; j < m.nq; ++j) qn[j] = qrow[j];
+      for (int i = 0; i < m.n_passive; ++i) {
+        const int j = m.passive_q[i];
+        qn[j] = it > 0 ? clampq(qrow[j], m.lo[j], m.hi[j]) : qrow[j];
+      }
+      qn[m.root_q] = qc[0];
+      for (int arm = 0; arm < 2; ++arm)
+        for (int k = 0; k < kArmDof; ++k) qn[m.arm_q[arm][k]] = qa[arm][k];
+      if (!emu_collide(m, *col, qn, tg)) {
+        conv = true;
+        break;
+      }
     }
     T A[2][6][8], u[2][6], v[2][6], al[2], be[2], dq[6], q_old[2][7];
     for (int arm = 0; arm < 2; ++arm) {
@@ -83,9 +113,16 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
 
 template <typename T>
 void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t stride, int64_t B,
-         const ikg_params* p, void* q_out, uint8_t* conv, int32_t* iters, void* err, void* trace, int trace_len) {
+         const ikg_params* p, void* q_out, uint8_t* conv, int32_t* iters, void* err, void* trace, int trace_len,
+         const ikg_collision_desc* cd) {
   ikg::KModel<T> m;
   ikg::build_kmodel<T>(*d, m);
+  static thread_local ikg::KCollision<T> kc;
+  const ikg::KCollision<T>* col = nullptr;
+  if (cd && p->check_collision) {
+    ikg::build_kcollision<T>(*cd, kc);
+    col = &kc;
+  }
   ikg::KParams<T> prm{(T)p->eps, (T)p->dt, (T)p->lambda, p->max_iters};
   const bool special = p->variant != 99 && ikg::choose_spec(m) == 1;  // variant 99: force generic
   for (int64_t i = 0; i < B; ++i) {
@@ -94,21 +131,43 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
     T* tr = trace ? (T*)trace + (int64_t)2 * trace_len * i : nullptr;
     if (special)
       emu_one<T, ikg::SpecNextage>(m, prm, p->lambda > 0, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
-                                   (T*)err + 2 * i, tr, trace_len);
+                                   (T*)err + 2 * i, tr, trace_len, col);
     else
       emu_one<T, ikg::SpecGeneric>(m, prm, p->lambda > 0, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
-                                   (T*)err + 2 * i, tr, trace_len);
+                                   (T*)err + 2 * i, tr, trace_len, col);
   }
 }
 
 }  // namespace
 
+// cd may be NULL; it is used when p->check_collision is set.
 extern "C" int ikg_emu_solve(const ikg_model_desc* d, int dtype, const void* targets, const void* q0,
                              int64_t q0_stride, int64_t B, const ikg_params* p, void* q_out, uint8_t* conv,
-                             int32_t* iters, void* err, void* trace, int trace_len) {
+                             int32_t* iters, void* err, void* trace, int trace_len, const ikg_collision_desc* cd) {
   if (dtype == IKG_F64)
-    emu<double>(d, targets, q0, q0_stride, B, p, q_out, conv, iters, err, trace, trace_len);
+    emu<double>(d, targets, q0, q0_stride, B, p, q_out, conv, iters, err, trace, trace_len, cd);
   else
-    emu<float>(d, targets, q0, q0_stride, B, p, q_out, conv, iters, err, trace, trace_len);
+    emu<float>(d, targets, q0, q0_stride, B, p, q_out, conv, iters, err, trace, trace_len, cd);
+  return 0;
+}
+
+template <typename T>
+void emu_col(const ikg_model_desc* d, const ikg_collision_desc* cd, const void* q, const void* targets, int64_t B,
+             uint8_t* out) {
+  ikg::KModel<T> m;
+  ikg::build_kmodel<T>(*d, m);
+  static thread_local ikg::KCollision<T> kc;
+  ikg::build_kcollision<T>(*cd, kc);
+  for (int64_t i = 0; i < B; ++i)
+    out[i] = emu_collide(m, kc, (const T*)q + d->nq * i, (const T*)targets + 12 * i) ? 1 : 0;
+}
+
+// Collision query through the device stage functions (ikg_collision_batch on the CPU).
+extern "C" int ikg_emu_collision(const ikg_model_desc* d, const ikg_collision_desc* cd, int dtype, const void* q,
+                                 const void* targets, int64_t B, uint8_t* out) {
+  if (dtype == IKG_F64)
+    emu_col<double>(d, cd, q, targets, B, out);
+  else
+    emu_col<float>(d, cd, q, targets, B, out);
   return 0;
 }

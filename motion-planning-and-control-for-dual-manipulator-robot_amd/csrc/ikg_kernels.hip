@@ -74,26 +74,6 @@ __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams
   conv_out = conv;
 }
 
-// tools.getcubeplacement: oMcube * hook (tools.py:54-59), for this lane's arm.
-template <typename T>
-__device__ inline void hook_target(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ tg, T* RT,
-                                   T* tT) {
-  const bool right = arm != 0;
-  T CR[9], Ct[3], HR[9], Ht[3], d[3];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) CR[i] = tg[i];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) Ct[i] = tg[9 + i];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) HR[i] = sel(right, m->hook_R[1][i], m->hook_R[0][i]);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) Ht[i] = sel(right, m->hook_t[1][i], m->hook_t[0][i]);
-  matmul3(CR, HR, RT);
-  matvec3(CR, Ht, d);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) tT[i] = Ct[i] + d[i];
-}
-
 template <typename T>
 __device__ inline void load_q(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow, T& qc, T* qa) {
   qc = qrow[m->root_q];
@@ -319,6 +299,10 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   BatchArgs b{a.targets, a.seeds, a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
   hipError_t e = launch_pair_batch<T>(dmodel, prm, b, spec, s);
   if (e != hipSuccess) return e;
+  if (a.collision) {  // converged-but-colliding seeds keep iterating (inverse_geometry.py:70)
+    e = launch_collide_continue<T>(dmodel, (const KCollision<T>*)a.collision, prm, b, spec, s);
+    if (e != hipSuccess) return e;
+  }
   // 2) one wave per target picks the best seed
   const int block = 256;
   const dim3 grid((unsigned)((a.T * 64 + block - 1) / block));

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ikg_collision.hpp"
 #include "ikg_device.hpp"
 
 namespace ikg {
@@ -37,6 +38,9 @@ struct MultiArgs {
   uint8_t* ws_conv;
   int32_t* ws_iters;
   void* ws_err;
+  // KCollision<T>* (device) when params.check_collision: the seeds' results
+  // go through the collision continuation before the best-seed reduction
+  const void* collision = nullptr;
 };
 
 // kernel specialisation chosen at model creation (ikg_model_build.hpp)
@@ -62,5 +66,12 @@ hipError_t launch_pair_state(const KModel<T>* dm, const void* targets, const voi
                              void* out, hipStream_t s);
 
 
+template <typename T>
+hipError_t launch_collision(const KModel<T>* dm, const KCollision<T>* dc, const void* q, const void* targets,
+                            int64_t B, uint8_t* out, hipStream_t s);
+
+template <typename T>
+hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
+                                   const BatchArgs& a, int spec, hipStream_t s);
 
 }  // namespace ikg

@@ -2,8 +2,10 @@
 // (shared by the C-ABI and the host emulator).
 #pragma once
 
+#include <cmath>
 #include <cstring>
 
+#include "ikg_collision.hpp"
 #include "ikg_device.hpp"
 #include "ikgrasp.h"
 
@@ -47,6 +49,10 @@ inline void build_kmodel(const ikg_model_desc& d, KModel<T>& k) {
   for (int q = 0; q < d.nq; ++q) {
     k.lo[q] = (T)d.lower[q];
     k.hi[q] = (T)d.upper[q];
+    for (int i = 0; i < 9; ++i) k.jR[q][i] = (T)d.placement[q][i];
+    for (int i = 0; i < 3; ++i) k.jt[q][i] = (T)d.placement[q][9 + i];
+    k.jaxis[q] = d.axis[q];
+    k.jparent[q] = d.parent[q];
   }
   k.nq = d.nq;
   bool used[IKG_MAX_NQ] = {};
@@ -101,5 +107,35 @@ inline int choose_spec(const KModel<T>& k) {
   return 0;                                                                   // kSpecGeneric
 }
 
+
+// Collision scene tables (bounding radii padded so rounding never rejects a
+// touching pair).
+template <typename T>
+inline void build_kcollision(const ikg_collision_desc& d, KCollision<T>& c) {
+  std::memset(&c, 0, sizeof(c));
+  c.n_geoms = d.n_geoms;
+  c.n_pairs = d.n_pairs;
+  c.target_geom = d.target_geom;
+  for (int g = 0; g < d.n_geoms; ++g) {
+    for (int i = 0; i < 9; ++i) c.R[g][i] = (T)d.placement[g][i];
+    for (int i = 0; i < 3; ++i) c.t[g][i] = (T)d.placement[g][9 + i];
+    for (int i = 0; i < 3; ++i) c.dims[g][i] = (T)d.dims[g][i];
+    c.kind[g] = d.kind[g];
+    c.joint[g] = d.joint[g];
+    const double* h = d.dims[g];
+    double r;  // bounding sphere about the placement origin, padded for rounding
+    if (d.kind[g] == IKG_GEOM_SPHERE)
+      r = h[0];
+    else if (d.kind[g] == IKG_GEOM_CYLINDER)
+      r = std::sqrt(h[0] * h[0] + h[1] * h[1]);
+    else
+      r = std::sqrt(h[0] * h[0] + h[1] * h[1] + h[2] * h[2]);
+    c.brad[g] = (T)(r * (1.0 + 1e-6) + 1e-9);
+  }
+  for (int k = 0; k < d.n_pairs; ++k) {
+    c.pairs[k][0] = (int16_t)d.pairs[k][0];
+    c.pairs[k][1] = (int16_t)d.pairs[k][1];
+  }
+}
 
 }  // namespace ikg

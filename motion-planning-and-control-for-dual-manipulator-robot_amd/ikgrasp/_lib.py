@@ -11,6 +11,8 @@ import os
 import numpy as np
 
 IKG_MAX_NQ = 32
+IKG_MAX_GEOMS = 64
+IKG_MAX_PAIRS = 1024
 IKG_ARM_DOF = 6
 IKG_F64, IKG_F32 = 0, 1
 IKG_FLAG_HOST_POINTERS = 1
@@ -53,13 +55,27 @@ class Params(C.Structure):
         ("variant", C.c_int32),
         ("lambda_", C.c_double),
         ("problems_per_wave", C.c_int32),
-        ("reserved", C.c_int32),
+        ("check_collision", C.c_int32),
+    ]
+
+
+class CollisionDesc(C.Structure):
+    _fields_ = [
+        ("n_geoms", C.c_int32),
+        ("kind", C.c_int32 * IKG_MAX_GEOMS),
+        ("joint", C.c_int32 * IKG_MAX_GEOMS),
+        ("placement", (C.c_double * 12) * IKG_MAX_GEOMS),
+        ("dims", (C.c_double * 3) * IKG_MAX_GEOMS),
+        ("target_geom", C.c_int32),
+        ("n_pairs", C.c_int32),
+        ("pairs", (C.c_int32 * 2) * IKG_MAX_PAIRS),
     ]
 
 
 EXPORTS = [
     "ikg_model_create", "ikg_model_destroy", "ikg_params_default", "ikg_solve_batch",
     "ikg_solve_multistart", "ikg_fk_batch", "ikg_log6_batch", "ikg_last_error", "ikg_version",
+    "ikg_model_set_collision", "ikg_collision_batch",
 ]
 
 _lib = None
@@ -95,6 +111,10 @@ def load() -> C.CDLL:
     lib.ikg_fk_batch.restype = i32
     lib.ikg_log6_batch.argtypes = [i32, i32, vp, i64, vp, vp, C.c_uint32]
     lib.ikg_log6_batch.restype = i32
+    lib.ikg_model_set_collision.argtypes = [vp, C.POINTER(CollisionDesc)]
+    lib.ikg_model_set_collision.restype = i32
+    lib.ikg_collision_batch.argtypes = [vp, i32, i32, vp, vp, i64, vp, vp, C.c_uint32]
+    lib.ikg_collision_batch.restype = i32
     lib.ikg_last_error.argtypes = []
     lib.ikg_last_error.restype = C.c_char_p
     lib.ikg_version.argtypes = []
@@ -127,6 +147,28 @@ def model_desc(model) -> ModelDesc:
         d.arm_q[a][:] = [int(x) for x in model.arm_q[a]]
         d.hand[a][:] = _se3_12(model.hand_R[a], model.hand_t[a])
         d.hook[a][:] = _se3_12(model.hook_R[a], model.hook_t[a])
+    return d
+
+
+def collision_desc(scene) -> CollisionDesc:
+    """ikgrasp.collision.CollisionScene -> ikg_collision_desc."""
+    n, m = len(scene.geoms), len(scene.pairs)
+    if n > IKG_MAX_GEOMS or m > IKG_MAX_PAIRS:
+        raise ValueError(f"scene too large: {n} geometries / {m} pairs (max {IKG_MAX_GEOMS}/{IKG_MAX_PAIRS})")
+    d = CollisionDesc()
+    d.n_geoms = n
+    d.target_geom = -1
+    for g, geom in enumerate(scene.geoms):
+        d.kind[g] = int(geom.kind)
+        d.joint[g] = int(geom.joint)
+        d.placement[g][:] = _se3_12(geom.R, geom.t)
+        d.dims[g][:] = [float(x) for x in geom.dims]
+        if geom.target:
+            d.target_geom = g
+    d.n_pairs = m
+    for k, (a, b) in enumerate(np.asarray(scene.pairs).reshape(-1, 2)):
+        d.pairs[k][0] = int(a)
+        d.pairs[k][1] = int(b)
     return d
 
 

@@ -5,8 +5,11 @@ by the batched HIP kernel, plus the batched / multi-start APIs.
 
 Same name, positional order and return as the reference.  Differences that
 a caller can observe:
-  * `success` is the convergence test of :70 only; the collision term
-    (tools.py:25-35) is the next scope row (§8f-1) and is not evaluated;
+  * none in `success`: when the robot carries a collision scene (the default
+    from setuppinocchio) the stop test is :70's `errors pass and not
+    collision(q)`, iterating on while converged-but-colliding, and a final
+    colliding q is a failure (:97-98) — all inside the GPU continuation kernel;
+    with `scene=None` success is the convergence test only;
   * `viz` is updated once with the final q instead of every iteration.
 `qcurrent` is copied, never mutated (:49); the cube is left placed at
 `cubetarget` (:42, tools.py:62-68).
@@ -34,7 +37,9 @@ def computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None):
     R, t = as_rt(cubetarget)
     target = np.concatenate([R.reshape(9), t])[None, :]
     q0 = np.array(qcurrent, dtype=np.float64).copy()  # :49
-    sol = _solver_of(robot).solve(target, q0, dtype="f64", eps=EPSILON, dt=DT_IK, max_iters=MAX_ITERS)
+    solver = _solver_of(robot)
+    sol = solver.solve(target, q0, dtype="f64", eps=EPSILON, dt=DT_IK, max_iters=MAX_ITERS,
+                       check_collision=solver.scene is not None)
     q = sol.q[0].astype(np.float64)
     if viz is not None and hasattr(viz, "display"):  # :92-94, once with the final q
         viz.display(q)
@@ -43,9 +48,13 @@ def computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None):
 
 def computeqgrasppose_batch(robot, qcurrent, cubetargets, dtype="f64", **kw):
     """Batched API: cubetargets [B,12] / [B,4,4] / list of SE3; qcurrent [nq]
-    (broadcast) or [B,nq] -> (q [B,nq], success [B], iters [B])."""
+    (broadcast) or [B,nq] -> (q [B,nq], success [B], iters [B]).  `success`
+    includes the collision term when the robot has a scene (override with
+    check_collision=False)."""
     targets = pack_targets(cubetargets)
-    sol = _solver_of(robot).solve(targets, np.asarray(qcurrent), dtype=dtype, **kw)
+    solver = _solver_of(robot)
+    kw.setdefault("check_collision", solver.scene is not None)
+    sol = solver.solve(targets, np.asarray(qcurrent), dtype=dtype, **kw)
     return sol.q, sol.converged, sol.iters
 
 
@@ -53,5 +62,7 @@ def computeqgrasppose_multistart(robot, seeds, cubetargets, dtype="f64", **kw):
     """Multi-start API: seeds [S,nq] x targets -> best seed per target:
     (q [T,nq], success [T], best_seed [T])."""
     targets = pack_targets(cubetargets)
-    sol = _solver_of(robot).solve_multistart(targets, np.asarray(seeds), dtype=dtype, **kw)
+    solver = _solver_of(robot)
+    kw.setdefault("check_collision", solver.scene is not None)
+    sol = solver.solve_multistart(targets, np.asarray(seeds), dtype=dtype, **kw)
     return sol.q, sol.converged, sol.best_seed

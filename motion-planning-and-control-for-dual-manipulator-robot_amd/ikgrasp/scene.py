@@ -26,19 +26,28 @@ class _ModelView:
 
 
 class Robot:
-    def __init__(self, model: DualArmModel | None = None, device: int = 0):
+    def __init__(self, model: DualArmModel | None = None, device: int = 0, scene="nextage"):
+        """scene: a CollisionScene, "nextage" (the reference scene compiled by
+        tools/compile_model.py, only valid with the default model) or None."""
         self.ik_model = model if model is not None else load_nextage()
         self.model = _ModelView(self.ik_model)
         self.q0 = np.zeros(self.model.nq)
         self.device = device
         self.cube_placement = None
+        self.cube_default = CUBE_PLACEMENT  # the cube geometry's placement before any setcubeplacement
+        if isinstance(scene, str):
+            if model is not None:
+                raise ValueError("pass the CollisionScene of a custom model explicitly (or scene=None)")
+            from .collision import load_nextage_scene
+            scene = load_nextage_scene()
+        self.scene = scene
         self._solver = None
 
     @property
     def solver(self):
         if self._solver is None:
             from .solver import IKSolver
-            self._solver = IKSolver(self.ik_model, device=self.device)
+            self._solver = IKSolver(self.ik_model, device=self.device, scene=self.scene)
         return self._solver
 
 
@@ -54,10 +63,14 @@ class Cube:
 
 def setuppinocchio(device: int = 0):
     """Same return shape as setup_pinocchio.setuppinocchio: (robot, table,
-    obstacle, cube); table/obstacle are None (collision scene is §8f-1)."""
+    obstacle, cube).  table/obstacle are the scene's geometry records (their
+    collision geometry lives in robot.scene, as in the reference where
+    loadobject appends them to the robot's collision model)."""
     robot = Robot(device=device)
     cube = Cube(robot.ik_model)
-    return robot, None, None, cube
+    table = next((g for g in robot.scene.geoms if g.name.startswith("baseLink")), None)
+    obstacle = next((g for g in robot.scene.geoms if g.name.startswith("obstaclebase")), None)
+    return robot, table, obstacle, cube
 
 
 def setupik(device: int = 0):

@@ -50,7 +50,8 @@ class Solution:
 class IKSolver:
     """Owns one native model (`ikg_model_create`)."""
 
-    def __init__(self, model: DualArmModel | None = None, device: int = 0):
+    def __init__(self, model: DualArmModel | None = None, device: int = 0, scene=None):
+        """`scene`: an ikgrasp.collision.CollisionScene to attach (see set_collision)."""
         self.lib = _lib.load()
         self.model = model if model is not None else load_nextage()
         self.desc = _lib.model_desc(self.model)
@@ -58,6 +59,16 @@ class IKSolver:
         _lib.check(self.lib.ikg_model_create(C.byref(self.desc), C.byref(h)))
         self._h = h
         self.device = device
+        self.scene = None
+        if scene is not None:
+            self.set_collision(scene)
+
+    def set_collision(self, scene):
+        """Attach the collision scene (ikg_model_set_collision); enables
+        `check_collision=True` solves and `collision()` queries."""
+        self._cdesc = _lib.collision_desc(scene)
+        _lib.check(self.lib.ikg_model_set_collision(self._h, C.byref(self._cdesc)))
+        self.scene = scene
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -74,9 +85,12 @@ class IKSolver:
     def nq(self) -> int:
         return self.model.nq
 
-    def params(self, eps=1e-3, dt=1e-2, max_iters=1000, lam=0.0, variant=_lib.IKG_VARIANT_AUTO, ppw=0):
+    def params(self, eps=1e-3, dt=1e-2, max_iters=1000, lam=0.0, variant=_lib.IKG_VARIANT_AUTO, ppw=0,
+               check_collision=False):
+        """check_collision: reference `success` (converged AND collision-free,
+        iterating on while converged-but-colliding, inverse_geometry.py:70)."""
         return _lib.default_params(eps=eps, dt=dt, max_iters=max_iters, lambda_=lam, variant=variant,
-                                   problems_per_wave=ppw)
+                                   problems_per_wave=ppw, check_collision=int(bool(check_collision)))
 
     # ------------------------------------------------------------------ batch
     def solve(self, targets, q0, dtype="f64", stream=None, **kw) -> Solution:
@@ -158,6 +172,28 @@ class IKSolver:
             q_out.ctypes.data, conv.ctypes.data, iters.ctypes.data, err.ctypes.data, best.ctypes.data, None,
             _lib.IKG_FLAG_HOST_POINTERS))
         return Solution(q_out, conv.astype(bool), iters, err, best)
+
+    # ------------------------------------------------------------------ collision
+    def collision(self, q, targets, dtype="f64"):
+        """tools.collision(robot, q) with the cube at each target: q [B,nq],
+        targets [B,12] -> bool [B] (numpy) or uint8 tensor (torch, device)."""
+        if _is_torch(q):
+            import torch
+            code, _ = _dtype(q.dtype)
+            qq = q.contiguous().view(-1, self.nq)
+            tg = targets.to(device=q.device, dtype=q.dtype).contiguous().view(-1, 12)
+            out = torch.empty(qq.shape[0], dtype=torch.uint8, device=q.device)
+            s = torch.cuda.current_stream(q.device).cuda_stream
+            _lib.check(self.lib.ikg_collision_batch(self._h, q.device.index or 0, code, qq.data_ptr(), tg.data_ptr(),
+                                                    qq.shape[0], out.data_ptr(), C.c_void_p(s), 0))
+            return out
+        code, npt = _dtype(dtype)
+        qq = np.ascontiguousarray(q, dtype=npt).reshape(-1, self.nq)
+        tg = np.ascontiguousarray(np.broadcast_to(np.asarray(targets, dtype=npt).reshape(-1, 12), (qq.shape[0], 12)))
+        out = np.empty(qq.shape[0], dtype=np.uint8)
+        _lib.check(self.lib.ikg_collision_batch(self._h, self.device, code, qq.ctypes.data, tg.ctypes.data,
+                                                qq.shape[0], out.ctypes.data, None, _lib.IKG_FLAG_HOST_POINTERS))
+        return out.astype(bool)
 
     # ------------------------------------------------------------------ log6
     def log6(self, M, dtype="f64") -> np.ndarray:

@@ -1,7 +1,8 @@
 """Mirror of the reference helpers on the IK path (tools.py).
 
-Same names and argument meaning.  `collision`/`distanceToObstacle` belong to
-the next scope row and are not provided yet: calling them
+Same names and argument meaning.  `collision` runs the HIP collision kernel
+(ikg_collision_batch) on the robot's scene with the cube at its current
+placement; `distanceToObstacle` is out of the current scope and
 raises NotImplementedError rather than silently answering.
 """
 from __future__ import annotations
@@ -47,8 +48,15 @@ def setcubeplacement(robot, cube, oMf):
 
 
 def collision(robot, q):
-    raise NotImplementedError("collision checking is the next scope row (SURVEY §8f-1); "
-                              "computeqgrasppose reports convergence-only success")
+    """tools.py:25-35 — True if any active pair of the scene intersects at q
+    (the cube geometry sits where setcubeplacement last put it)."""
+    solver = robot.solver
+    if solver.scene is None:
+        raise RuntimeError("robot has no collision scene attached (ikgrasp.scene.setuppinocchio builds it)")
+    placement = robot.cube_placement if robot.cube_placement is not None else robot.cube_default
+    R, t = as_rt(placement)
+    target = np.concatenate([R.reshape(9), t])[None, :]
+    return bool(solver.collision(np.asarray(q, dtype=np.float64).reshape(1, -1), target)[0])
 
 
 def distanceToObstacle(robot, q):

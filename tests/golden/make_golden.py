@@ -12,6 +12,13 @@
    are read off q0/qe_error_charts.png.
 2. `oracle_cases.npz` — seeded synthetic cases solved by the numpy oracle
    (oracle/ik_oracle.py, itself pinned to the KATs): inputs and outputs.
+3. `collision_scene.json` — the collision scene as parsed by the oracle's own
+   reader (oracle/collision_oracle.parse_scene) from the reference URDF/SRDF.
+4. `collision_cases.npz` — tools.collision queries (q, cube target) answered by
+   the collision oracle, with robustness flags (same answer with every
+   geometry inflated and deflated by 1e-9 m / 1e-4 m).
+5. `collision_solve_cases.npz` — computeqgrasppose WITH the collision term
+   (collision_oracle.computeqgrasppose) on the oracle_cases inputs.
 """
 import json
 import os
@@ -25,6 +32,7 @@ ROOT = os.path.abspath(os.path.join(HERE, "..", ".."))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd"))
 
+from oracle import collision_oracle  # noqa: E402
 from oracle import ik_oracle  # noqa: E402
 from ikgrasp.workload import uniform_targets, random_seeds  # noqa: E402
 from ikgrasp.model import load_nextage  # noqa: E402
@@ -88,7 +96,93 @@ def make_oracle_cases(n_uniform=48, n_yaw=24, n_seeded=24):
           "converged", sum(r[1] for r in res), "/", len(res))
 
 
+_SCENE = None
+
+
+def _scene():
+    global _SCENE
+    if _SCENE is None:
+        _SCENE = collision_oracle.load_scene(os.path.join(HERE, "collision_scene.json"))
+    return _SCENE
+
+
+def _scaled(scene, delta):
+    out = {"geoms": [dict(g) for g in scene["geoms"]], "pairs": scene["pairs"]}
+    for g in out["geoms"]:
+        g["dims"] = np.maximum(g["dims"] + delta * (g["dims"] > 0), 0.0)
+    return out
+
+
+def _query(args):
+    q, target = args
+    sc = _scene()
+    R, t = target[:9].reshape(3, 3), target[9:]
+    res = [collision_oracle.collision(sc, q, R, t)]
+    for d in (1e-9, 1e-4):
+        res.append(collision_oracle.collision(_scaled(sc, d), q, R, t) ==
+                   collision_oracle.collision(_scaled(sc, -d), q, R, t))
+    return res
+
+
+def make_collision_scene():
+    scene = collision_oracle.parse_scene(REF)
+    with open(os.path.join(HERE, "collision_scene.json"), "w") as f:
+        json.dump(scene, f, indent=1)
+    print("wrote collision_scene.json:", len(scene["geoms"]), "geometries,", len(scene["pairs"]), "pairs")
+
+
+def make_collision_cases(n_random=512):
+    m = load_nextage()
+    c = np.load(os.path.join(HERE, "oracle_cases.npz"))
+    kat = json.load(open(os.path.join(HERE, "kat.json")))
+    qs, tg, src = [], [], []
+    cp = np.concatenate([np.eye(3).reshape(9), kat["cube_placement"]["t"]])
+    cpt = np.concatenate([np.eye(3).reshape(9), kat["cube_placement_target"]["t"]])
+    for q, t in ((np.zeros(15), cp), (np.array(kat["q0"]), cp), (np.array(kat["qe"]), cpt)):
+        qs.append(q), tg.append(t), src.append(0)  # KAT-5 and the KAT solutions
+    for i in range(len(c["q"])):  # oracle solutions and the straight path from their seed
+        for f in np.linspace(0.1, 1.0, 10):
+            qs.append(c["q0"][i] + f * (c["q"][i] - c["q0"][i])), tg.append(c["targets"][i]), src.append(1)
+    rng = np.random.default_rng(300)
+    tr = uniform_targets(n_random, seed=301)
+    for i in range(n_random):
+        qs.append(rng.uniform(m.lower, m.upper)), tg.append(tr[i]), src.append(2)
+    qs, tg = np.array(qs), np.array(tg)
+    with Pool(8) as p:
+        res = np.array(p.map(_query, list(zip(qs, tg)), chunksize=8))
+    np.savez_compressed(os.path.join(HERE, "collision_cases.npz"), q=qs, targets=tg, source=np.array(src, np.int8),
+                        collision=res[:, 0], robust64=res[:, 1], robust32=res[:, 2])
+    print("wrote collision_cases.npz:", len(qs), "queries,", int(res[:, 0].sum()), "colliding,",
+          int((~res[:, 1]).sum()), "fp64-boundary,", int((~res[:, 2]).sum()), "fp32-boundary")
+
+
+def _solve_col(args):
+    target, q0 = args
+    q, ok, it, (nl, nr) = collision_oracle.computeqgrasppose(_scene(), q0, target[:9].reshape(3, 3), target[9:])
+    return q, ok, it, nl, nr
+
+
+def make_collision_solve_cases():
+    c = np.load(os.path.join(HERE, "oracle_cases.npz"))
+    with Pool(8) as p:
+        res = p.map(_solve_col, list(zip(c["targets"], c["q0"])))
+    np.savez_compressed(
+        os.path.join(HERE, "collision_solve_cases.npz"), targets=c["targets"], q0=c["q0"],
+        q=np.array([r[0] for r in res]), success=np.array([r[1] for r in res]),
+        iters=np.array([r[2] for r in res], dtype=np.int32), err=np.array([[r[3], r[4]] for r in res]))
+    print("wrote collision_solve_cases.npz: success", sum(r[1] for r in res), "/", len(res),
+          "(convergence-only:", int(c["converged"].sum()), ")")
+
+
 if __name__ == "__main__":
-    if os.path.isdir(REF):
+    what = sys.argv[1:] or ["kat", "cases", "scene", "collision", "collision_solve"]
+    if os.path.isdir(REF) and "kat" in what:
         make_kats()
-    make_oracle_cases()
+    if "cases" in what:
+        make_oracle_cases()
+    if os.path.isdir(REF) and "scene" in what:
+        make_collision_scene()
+    if "collision" in what:
+        make_collision_cases()
+    if "collision_solve" in what:
+        make_collision_solve_cases()

@@ -1,0 +1,126 @@
+"""GPU parity of the collision term: ikg_collision_batch and the
+collision-continuation kernel against the collision oracle's fixtures
+(tests/golden/collision_*.npz, made by tests/golden/make_golden.py).
+
+Bars: collision booleans identical to the oracle on every fixture query
+that is not within 1e-9 m (fp64) / 1e-4 m (fp32) of touching (flags
+robust64/robust32, computed by re-running the oracle on inflated and deflated
+geometry); solves with check_collision: identical success flags and update
+counts, q within 1e-9 (fp64) of the oracle's loop.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def csolver():
+    from ikgrasp.collision import load_nextage_scene
+    from ikgrasp.solver import IKSolver
+    s = IKSolver(device=0, scene=load_nextage_scene())
+    yield s
+    s.close()
+
+
+@pytest.fixture(scope="module")
+def col_cases():
+    return dict(np.load(os.path.join(GOLDEN, "collision_cases.npz")))
+
+
+@pytest.fixture(scope="module")
+def solve_cases():
+    return dict(np.load(os.path.join(GOLDEN, "collision_solve_cases.npz")))
+
+
+def _row(d):
+    return np.concatenate([np.array(d["R"], dtype=np.float64).reshape(9), np.array(d["t"], dtype=np.float64)])
+
+
+def test_collision_batch_fp64(csolver, col_cases):
+    c = col_cases
+    got = csolver.collision(c["q"], c["targets"])
+    ok = c["robust64"].astype(bool)
+    assert np.array_equal(got[ok], c["collision"][ok])
+    assert got[0]  # KAT-5: collision(robot, robot.q0) is True
+
+
+def test_collision_batch_fp32(csolver, col_cases):
+    c = col_cases
+    got = csolver.collision(c["q"], c["targets"], dtype="f32")
+    ok = c["robust32"].astype(bool)
+    assert np.array_equal(got[ok], c["collision"][ok])
+
+
+def test_collision_batch_large_is_consistent(csolver, col_cases):
+    """4096 queries (the fixture set tiled): same answers per copy."""
+    c = col_cases
+    reps = 4096 // len(c["q"]) + 1
+    q = np.tile(c["q"], (reps, 1))[:4096]
+    tg = np.tile(c["targets"], (reps, 1))[:4096]
+    got = csolver.collision(q, tg)
+    base = np.tile(csolver.collision(c["q"], c["targets"]), reps)[:4096]
+    assert np.array_equal(got, base)
+
+
+def test_solve_with_collision_fp64(csolver, solve_cases, oracle_cases):
+    c = solve_cases
+    sol = csolver.solve(c["targets"], c["q0"], check_collision=True)
+    assert np.array_equal(sol.converged, c["success"])
+    assert np.array_equal(sol.iters, c["iters"])
+    s = c["success"]
+    assert np.abs(sol.q[s] - c["q"][s]).max() <= 1e-9
+    assert np.abs(sol.err[s] - c["err"][s]).max() <= 1e-10
+    cont = oracle_cases["converged"] & ~c["success"]  # converged but colliding -> ran on (:70)
+    assert cont.sum() >= 5 and (sol.iters[cont] == 1000).all()
+    # final iterate of those: same loop as the oracle (pinv drift only in the null space)
+    assert np.abs(sol.err[cont] - c["err"][cont]).max() <= 1e-9
+    # the final q collides (:97-98) for every failed-after-converging case
+    assert csolver.collision(sol.q[cont], c["targets"][cont]).all()
+
+
+def test_solve_with_collision_fp32(csolver, solve_cases):
+    c = solve_cases
+    sol = csolver.solve(c["targets"], c["q0"], dtype="f32", check_collision=True)
+    agree = (sol.converged == c["success"]).mean()
+    assert agree >= 0.95
+    both = sol.converged & c["success"]
+    assert (np.abs(sol.iters[both] - c["iters"][both]) <= 2).all()
+
+
+def test_dropin_uses_collision_and_reproduces_kats(kat):
+    import ikgrasp
+    from ikgrasp.config import CUBE_PLACEMENT, CUBE_PLACEMENT_TARGET
+    from ikgrasp.tools import collision
+    robot, table, obstacle, cube = ikgrasp.setuppinocchio()
+    assert robot.solver.scene is not None and table is not None and obstacle is not None
+    assert collision(robot, robot.q0)  # KAT-5 (lab_instructions.ipynb:252)
+    q0, ok0 = ikgrasp.computeqgrasppose(robot, robot.q0.copy(), cube, CUBE_PLACEMENT)
+    qe, oke = ikgrasp.computeqgrasppose(robot, robot.q0.copy(), cube, CUBE_PLACEMENT_TARGET)
+    assert ok0 and oke
+    assert np.abs(q0 - kat["q0"]).max() <= 1e-12 and np.abs(qe - kat["qe"]).max() <= 1e-12
+    assert not collision(robot, qe)
+
+
+def test_multistart_with_collision_matches_single_solves(csolver, solve_cases):
+    c = solve_cases
+    tg = c["targets"][:16]
+    seeds = np.stack([np.zeros(15)] + [c["q0"][-k] for k in range(1, 4)])
+    ms = csolver.solve_multistart(tg, seeds, check_collision=True)
+    per = [csolver.solve(tg, s, check_collision=True) for s in seeds]
+    for t in range(len(tg)):
+        b = ms.best_seed[t]
+        assert ms.converged[t] == per[b].converged[t]
+        assert ms.converged[t] == any(p.converged[t] for p in per)
+        assert np.array_equal(ms.q[t], per[b].q[t])
+
+
+def test_check_collision_without_scene_fails_loudly(solver):
+    from ikgrasp._lib import IkgError
+    with pytest.raises(IkgError, match="collision scene"):
+        solver.solve(np.concatenate([np.eye(3).reshape(9), [0.4, 0.1, 0.93]])[None], np.zeros(15),
+                     check_collision=True)

@@ -22,7 +22,7 @@ def emu():
         pytest.skip("libikgrasp_emu.so not built")
     lib = C.CDLL(EMU)
     vp = C.c_void_p
-    lib.ikg_emu_solve.argtypes = [vp, C.c_int, vp, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, vp, C.c_int]
+    lib.ikg_emu_solve.argtypes = [vp, C.c_int, vp, vp, C.c_int64, C.c_int64, vp, vp, vp, vp, vp, vp, C.c_int, vp]
     desc = _lib.model_desc(load_nextage())
 
     def solve(targets, q0, dtype=0, **kw):
@@ -36,7 +36,7 @@ def emu():
         it = np.empty(B, np.int32)
         err = np.empty((B, 2), npt)
         lib.ikg_emu_solve(C.byref(desc), dtype, tg.ctypes.data, q0.ctypes.data, 15, B, C.byref(p), q.ctypes.data,
-                          conv.ctypes.data, it.ctypes.data, err.ctypes.data, None, 0)
+                          conv.ctypes.data, it.ctypes.data, err.ctypes.data, None, 0, None)
         return q, conv.astype(bool), it, err
 
     return solve

@@ -15,7 +15,9 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(HERE, "..", "motion-planning-and-control-for-dual-manipulator-robot_amd"))
 
+from ikgrasp.collision import NEXTAGE_COLLISION_JSON, build_scene  # noqa: E402
 from ikgrasp.model import DualArmModel, NEXTAGE_JSON  # noqa: E402
+from ikgrasp.se3 import rotate  # noqa: E402
 
 
 def main(ref="/root/reference"):
@@ -27,6 +29,18 @@ def main(ref="/root/reference"):
     with open(NEXTAGE_JSON, "w") as f:
         f.write(m.to_json())
     print(f"wrote {NEXTAGE_JSON}: nq={m.nq} root={m.root_q} arms={m.arm_q.tolist()}")
+    # collision scene (setup_pinocchio.py:53-83; placements config.py:33-37)
+    urdf = os.path.join(ref, "models/nextagea_description/urdf")
+    scene = build_scene(
+        os.path.join(urdf, "NextageaOpen.urdf"), os.path.join(urdf, "NextageAOpen.srdf"),
+        os.path.join(ref, "models/table/table_tallerscaled.urdf"), os.path.join(ref, "models/cubes/obstacle.urdf"),
+        cube, m.joint_names, base,
+        (rotate("z", -np.pi / 2), np.array([0.8, 0.0, 0.0])),
+        (rotate("z", 0.0), np.array([0.43, -0.1, 0.94])),
+        (rotate("z", 0.0), np.array([0.33, -0.3, 0.93])))
+    with open(NEXTAGE_COLLISION_JSON, "w") as f:
+        f.write(scene.to_json())
+    print(f"wrote {NEXTAGE_COLLISION_JSON}: {len(scene.geoms)} geometries, {len(scene.pairs)} pairs")
 
 
 if __name__ == "__main__":
