@@ -75,6 +75,10 @@ def main():
     ap.add_argument("--multistart", type=int, default=0,
                     help="seeds per target (BASELINE configs[4]): every target solved from S random seeds, "
                          "best seed kept; value counts converged targets/s")
+    ap.add_argument("--collision", action="store_true",
+                    help="reference `success` with the collision term (inverse_geometry.py:70, :97-98): "
+                         "converged-but-colliding problems iterate on in the continuation kernel; "
+                         "value counts collision-free converged solves/s")
     args = ap.parse_args()
 
     import torch
@@ -92,7 +96,11 @@ def main():
     from ikgrasp.solver import IKSolver
     from ikgrasp.workload import random_seeds, uniform_targets
 
-    solver = IKSolver(device=local)
+    scene = None
+    if args.collision:
+        from ikgrasp.collision import load_nextage_scene
+        scene = load_nextage_scene()
+    solver = IKSolver(device=local, scene=scene)
     B = args.batch
     tg_np = uniform_targets(B, seed=rank, yaw=args.yaw)
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
@@ -117,9 +125,11 @@ def main():
         if ev is not None:
             ev[0].record(stream)
         if S:
-            solver.solve_multistart_into(targets, seeds, q_out, conv, iters, err, best, code, sh)
+            solver.solve_multistart_into(targets, seeds, q_out, conv, iters, err, best, code, sh,
+                                         check_collision=args.collision)
         else:
-            solver.solve_into(targets, q0, q_out, conv, iters, err, code, sh, variant=args.variant)
+            solver.solve_into(targets, q0, q_out, conv, iters, err, code, sh, variant=args.variant,
+                              check_collision=args.collision)
         if ev is not None:
             ev[1].record(stream)
         if world > 1 and not args.no_gather:
@@ -174,7 +184,9 @@ def main():
                 "workload": (f"BASELINE configs[4]: multi-start {S} seeds x {B} targets per GPU, {args.dtype}"
                              if S else
                              f"BASELINE configs[1]: batch {B} grasp targets per GPU, {args.dtype}, "
-                             f"pair kernel (2 lanes/problem)"),
+                             f"pair kernel (2 lanes/problem)") +
+                            (" + collision term (continuation kernel)" if args.collision else ""),
+                "collision_term": bool(args.collision),
                 "seeds_per_target": S or 1,
                 "batch_per_gpu": B, "global_batch": B * world, "yaw_range": args.yaw,
                 "parallelism": f"shard{world}" + ("" if world == 1 or args.no_gather else "+rccl_gather_q"),
@@ -185,7 +197,8 @@ def main():
             "roofline": {
                 "bound": "valu", "achieved": flops, "peak": PEAK_VALU[args.dtype], "unit": "TFLOP/s",
                 "frac": flops / PEAK_VALU[args.dtype] if flops else None, "traffic": traffic,
-                "kernel": "ikg_pair_batch_kernel", "kernel_ms": kern_ms,
+                "kernel": "ikg_pair_batch_kernel" + (" + ikg_collide_continue_kernel" if args.collision else ""),
+                "kernel_ms": kern_ms,
                 "work": f"sum(iters)={sum_iters} x {F_ITER} FP ops (SURVEY §8a)",
             },
             "roofline_hbm": {
@@ -194,7 +207,7 @@ def main():
                 "algorithmic_bytes": abytes,
             },
         }
-        if world == 1 and not args.no_cpu_baseline and not S:
+        if world == 1 and not args.no_cpu_baseline and not S and not args.collision:
             out["cpu_baseline"] = cpu_baseline(tg_np)
         print(json.dumps(out), flush=True)
     if world > 1:

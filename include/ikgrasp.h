@@ -121,14 +121,16 @@ int ikg_model_set_collision(ikg_model* model, const ikg_collision_desc* desc);
 void ikg_params_default(ikg_params* p);
 
 /*
- * Batched computeqgrasppose (inverse_geometry.py:17-100, collision term
- * excluded — see DESIGN.md §8f-1).
+ * Batched computeqgrasppose (inverse_geometry.py:17-100).  With
+ * params->check_collision = 1 (needs ikg_model_set_collision) the stop test is
+ * the reference's `errors pass and not collision(q)` (:70) and a final
+ * colliding q is a failure (:97-98); with 0 it is the error test only.
  *   targets   [B,12]  cube placements (cubetarget); hooks are applied inside
  *   q0        [B,nq] (q0_stride = nq) or [nq] broadcast (q0_stride = 0)
  *   q_out     [B,nq]  first iterate with both errors < eps, else the iterate
  *                     after max_iters updates (same as the reference)
- *   converged [B]     1 if the stop test passed (reference `success` without
- *                     the collision term)
+ *   converged [B]     1 if the stop test passed (the reference `success`
+ *                     when check_collision = 1)
  *   iters     [B]     joint updates performed (may be NULL)
  *   err_out   [B,2]   |log6| of left/right hand at q_out (may be NULL)
  */

@@ -38,9 +38,22 @@ struct KCollision {
 template <typename T>
 struct CollideScratch {
   T q[kMaxNq];
+  T sn[kMaxNq];      // sin / cos of q (filled by the caller or by collide_wave)
+  T cs[kMaxNq];
+  int32_t par[kMaxNq];  // jparent staged in LDS
   T L[kMaxNq][12];   // joint-local transforms placement * R_axis(q)
   T F[kMaxNq][12];   // world joint frames
   T P[kMaxGeoms][12];  // world geometry placements
+};
+
+// Witness of the previous check of one problem (LDS): the colliding pair and,
+// when its GJK ended on an enclosing tetrahedron, the 4 search directions.
+template <typename T>
+struct Witness {
+  int32_t pair;     // -1: none
+  int32_t cert_ok;  // dir[] valid
+  T dir[12];
+  T pts[4][3];
 };
 
 template <typename T>
@@ -83,134 +96,179 @@ IKG_HD inline void triple(const T* a, const T* b, const T* c, T* out) {  // (a x
 }
 
 // Boolean GJK: do the convex shapes intersect (origin inside A - B)?
+// The simplex lives in named registers (s1..s3 = older vertices, oldest
+// first; `a` = newest); every case below indexes them statically, so nothing
+// spills to scratch.  Each vertex carries the search direction that produced
+// it, so an enclosing tetrahedron can be handed back as a certificate: the
+// four directions whose support points, re-evaluated at nearby poses, are
+// checked for enclosure first (tetra_encloses_origin) before a fresh GJK.
 template <typename T>
-IKG_HD inline bool gjk_intersect(const Shape<T>& A, const Shape<T>& B) {
-  T sim[4][3];
-  int n;
+struct GVert {
+  T p[3];  // support point of A - B
+  T d[3];  // direction it was taken in
+};
+
+template <typename T>
+IKG_HD inline void cp3(T* d, const T* s) {
+  d[0] = s[0];
+  d[1] = s[1];
+  d[2] = s[2];
+}
+
+// [s1, a]: keep the segment or drop to {a}.  Returns true if the origin is on it.
+template <typename T>
+IKG_HD inline bool gjk_line(const GVert<T>& a, GVert<T>& s1, GVert<T>& s2, int& m, T* dir) {
+  const T ao[3] = {-a.p[0], -a.p[1], -a.p[2]};
+  const T ab[3] = {s1.p[0] - a.p[0], s1.p[1] - a.p[1], s1.p[2] - a.p[2]};
+  if (dot3(ab, ao) > T(0)) {
+    s2 = a;
+    m = 2;
+    triple(ab, ao, ab, dir);
+    return dot3(dir, dir) < T(1e-30);
+  }
+  s1 = a;
+  m = 1;
+  cp3(dir, ao);
+  return false;
+}
+
+// [s1 = c, s2 = b, a]
+template <typename T>
+IKG_HD inline bool gjk_triangle(const GVert<T>& a, GVert<T>& s1, GVert<T>& s2, GVert<T>& s3, int& m, T* dir) {
+  const T ao[3] = {-a.p[0], -a.p[1], -a.p[2]};
+  T ab[3], ac[3], abc[3], t1[3];
+  for (int i = 0; i < 3; ++i) {
+    ab[i] = s2.p[i] - a.p[i];
+    ac[i] = s1.p[i] - a.p[i];
+  }
+  cross3(ab, ac, abc);
+  cross3(abc, ac, t1);
+  if (dot3(t1, ao) > T(0)) {
+    if (dot3(ac, ao) > T(0)) {  // keep [c, a]
+      s2 = a;
+      m = 2;
+      triple(ac, ao, ac, dir);
+      return dot3(dir, dir) < T(1e-30);
+    }
+    s1 = s2;  // line [b, a]
+    return gjk_line(a, s1, s2, m, dir);
+  }
+  cross3(ab, abc, t1);
+  if (dot3(t1, ao) > T(0)) {
+    s1 = s2;  // line [b, a]
+    return gjk_line(a, s1, s2, m, dir);
+  }
+  if (dot3(abc, ao) > T(0)) {  // [c, b, a]
+    cp3(dir, abc);
+  } else {  // [b, c, a]
+    const GVert<T> tmp = s1;
+    s1 = s2;
+    s2 = tmp;
+    for (int i = 0; i < 3; ++i) dir[i] = -abc[i];
+  }
+  s3 = a;
+  m = 3;
+  return false;
+}
+
+// [s1 = d, s2 = c, s3 = b, a]; returns 2 when the tetrahedron encloses the origin.
+template <typename T>
+IKG_HD inline int gjk_tetra(const GVert<T>& a, GVert<T>& s1, GVert<T>& s2, GVert<T>& s3, int& m, T* dir) {
+  const T ao[3] = {-a.p[0], -a.p[1], -a.p[2]};
+  T ab[3], ac[3], ad[3], f[3];
+  for (int i = 0; i < 3; ++i) {
+    ab[i] = s3.p[i] - a.p[i];
+    ac[i] = s2.p[i] - a.p[i];
+    ad[i] = s1.p[i] - a.p[i];
+  }
+  cross3(ab, ac, f);
+  if (dot3(f, ao) > T(0)) {  // triangle [c, b, a]
+    s1 = s2;
+    s2 = s3;
+    return gjk_triangle(a, s1, s2, s3, m, dir) ? 1 : 0;
+  }
+  cross3(ac, ad, f);
+  if (dot3(f, ao) > T(0)) return gjk_triangle(a, s1, s2, s3, m, dir) ? 1 : 0;  // triangle [d, c, a]
+  cross3(ad, ab, f);
+  if (dot3(f, ao) > T(0)) {  // triangle [b, d, a]
+    s2 = s1;
+    s1 = s3;
+    return gjk_triangle(a, s1, s2, s3, m, dir) ? 1 : 0;
+  }
+  return 2;  // origin enclosed
+}
+
+template <typename T>
+IKG_HD inline void mink_support(const Shape<T>& A, const Shape<T>& B, const T* dir, T* out) {
+  T pa[3], pb[3], nd[3] = {-dir[0], -dir[1], -dir[2]};
+  shape_support(A, dir, pa);
+  shape_support(B, nd, pb);
+  for (int i = 0; i < 3; ++i) out[i] = pa[i] - pb[i];
+}
+
+// 0: separated; 1: intersecting; 2: intersecting with `cert` (12 values = the
+// 4 search directions of an origin-enclosing tetrahedron) filled when non-null.
+template <typename T>
+IKG_HD inline int gjk_intersect(const Shape<T>& A, const Shape<T>& B, T* cert = nullptr) {
+  GVert<T> s1, s2, s3, a;
   T d[3] = {A.t[0] - B.t[0], A.t[1] - B.t[1], A.t[2] - B.t[2]};
   if (dot3(d, d) == T(0)) d[0] = T(1);
-  auto sup = [&](const T* dir, T* out) {
-    T pa[3], pb[3], nd[3] = {-dir[0], -dir[1], -dir[2]};
-    shape_support(A, dir, pa);
-    shape_support(B, nd, pb);
-    for (int i = 0; i < 3; ++i) out[i] = pa[i] - pb[i];
-  };
-  sup(d, sim[0]);
-  n = 1;
-  for (int i = 0; i < 3; ++i) d[i] = -sim[0][i];
+  cp3(s1.d, d);
+  mink_support(A, B, d, s1.p);
+  int m = 1;
+  for (int i = 0; i < 3; ++i) d[i] = -s1.p[i];
   for (int iter = 0; iter < kGjkIters; ++iter) {
-    if (dot3(d, d) < T(1e-30)) return true;
-    T a[3];
-    sup(d, a);
-    if (dot3(a, d) < T(0)) return false;  // separating direction
-    for (int i = 0; i < 3; ++i) sim[n][i] = a[i];
-    ++n;
-    // ---- reduce the simplex towards the origin (a = newest point)
-    for (int pass = 0; pass < 3; ++pass) {
-      const T* A0 = sim[n - 1];
-      T ao[3] = {-A0[0], -A0[1], -A0[2]};
-      if (n == 2) {
-        T ab[3] = {sim[0][0] - A0[0], sim[0][1] - A0[1], sim[0][2] - A0[2]};
-        if (dot3(ab, ao) > T(0)) {
-          triple(ab, ao, ab, d);
-          if (dot3(d, d) < T(1e-30)) return true;  // origin on the segment
-        } else {
-          for (int i = 0; i < 3; ++i) sim[0][i] = A0[i];
-          n = 1;
-          for (int i = 0; i < 3; ++i) d[i] = ao[i];
-        }
-        break;
-      }
-      if (n == 3) {
-        T ab[3], ac[3], abc[3], t1[3];
-        for (int i = 0; i < 3; ++i) {
-          ab[i] = sim[1][i] - A0[i];
-          ac[i] = sim[0][i] - A0[i];
-        }
-        cross3(ab, ac, abc);
-        cross3(abc, ac, t1);
-        if (dot3(t1, ao) > T(0)) {
-          if (dot3(ac, ao) > T(0)) {  // keep [c, a]
-            for (int i = 0; i < 3; ++i) sim[1][i] = A0[i];
-            n = 2;
-            triple(ac, ao, ac, d);
-            if (dot3(d, d) < T(1e-30)) return true;
-            break;
-          }
-          for (int i = 0; i < 3; ++i) {  // line [b, a]
-            sim[0][i] = sim[1][i];
-            sim[1][i] = A0[i];
-          }
-          n = 2;
-          continue;
-        }
-        cross3(ab, abc, t1);
-        if (dot3(t1, ao) > T(0)) {
-          for (int i = 0; i < 3; ++i) {
-            sim[0][i] = sim[1][i];
-            sim[1][i] = A0[i];
-          }
-          n = 2;
-          continue;
-        }
-        if (dot3(abc, ao) > T(0)) {
-          for (int i = 0; i < 3; ++i) d[i] = abc[i];  // [c, b, a]
-        } else {
-          for (int i = 0; i < 3; ++i) {  // [b, c, a]
-            const T tmp = sim[0][i];
-            sim[0][i] = sim[1][i];
-            sim[1][i] = tmp;
-            d[i] = -abc[i];
-          }
-        }
-        break;
-      }
-      // n == 4: sim = [d, c, b, a]
-      T ab[3], ac[3], ad[3], f[3];
-      for (int i = 0; i < 3; ++i) {
-        ab[i] = sim[2][i] - A0[i];
-        ac[i] = sim[1][i] - A0[i];
-        ad[i] = sim[0][i] - A0[i];
-      }
-      cross3(ab, ac, f);
-      if (dot3(f, ao) > T(0)) {  // triangle [c, b, a]
-        for (int i = 0; i < 3; ++i) {
-          sim[0][i] = sim[1][i];
-          sim[1][i] = sim[2][i];
-          sim[2][i] = A0[i];
-        }
-        n = 3;
-        continue;
-      }
-      cross3(ac, ad, f);
-      if (dot3(f, ao) > T(0)) {  // triangle [d, c, a]
-        for (int i = 0; i < 3; ++i) sim[2][i] = A0[i];
-        n = 3;
-        continue;
-      }
-      cross3(ad, ab, f);
-      if (dot3(f, ao) > T(0)) {  // triangle [b, d, a]
-        for (int i = 0; i < 3; ++i) {
-          sim[1][i] = sim[0][i];
-          sim[0][i] = sim[2][i];
-          sim[2][i] = A0[i];
-        }
-        n = 3;
-        continue;
-      }
-      return true;  // origin enclosed
+    if (dot3(d, d) < T(1e-30)) return 1;
+    cp3(a.d, d);
+    mink_support(A, B, d, a.p);
+    if (dot3(a.p, d) < T(0)) return 0;  // separating direction
+    int in;
+    if (m == 1)
+      in = gjk_line(a, s1, s2, m, d) ? 1 : 0;
+    else if (m == 2)
+      in = gjk_triangle(a, s1, s2, s3, m, d) ? 1 : 0;
+    else
+      in = gjk_tetra(a, s1, s2, s3, m, d);
+    if (in == 2 && cert) {
+      cp3(cert, s1.d);
+      cp3(cert + 3, s2.d);
+      cp3(cert + 6, s3.d);
+      cp3(cert + 9, a.d);
     }
+    if (in) return in;
   }
-  return true;  // iteration cap: treat as touching
+  return 1;  // iteration cap: treat as touching
+}
+
+// Strict origin-in-tetrahedron test (barycentric signs): a certificate that
+// the convex set holding the four points, here A - B, contains the origin.
+template <typename T>
+IKG_HD inline bool tetra_encloses_origin(const T* P0, const T* P1, const T* P2, const T* P3) {
+  auto vol = [](const T* a, const T* b, const T* c, const T* d) {
+    T u[3], v[3], w[3], x[3];
+    for (int i = 0; i < 3; ++i) {
+      u[i] = b[i] - a[i];
+      v[i] = c[i] - a[i];
+      w[i] = d[i] - a[i];
+    }
+    cross3(u, v, x);
+    return dot3(x, w);
+  };
+  const T O[3] = {T(0), T(0), T(0)};
+  const T V = vol(P0, P1, P2, P3);
+  if (V == T(0)) return false;
+  return vol(O, P1, P2, P3) * V > T(0) && vol(P0, O, P2, P3) * V > T(0) && vol(P0, P1, O, P3) * V > T(0) &&
+         vol(P0, P1, P2, O) * V > T(0);
 }
 
 // Narrow phase of one pair (hpp-fcl collide(): intersection <=> collision).
+// `cert` as for gjk_intersect (only GJK pairs produce one).
 template <typename T>
-IKG_HD inline bool pair_collides(const Shape<T>& A, const Shape<T>& B) {
+IKG_HD inline int pair_collides(const Shape<T>& A, const Shape<T>& B, T* cert = nullptr) {
   if (A.kind == kSphere && B.kind == kSphere) {
     T d[3] = {A.t[0] - B.t[0], A.t[1] - B.t[1], A.t[2] - B.t[2]};
     const T r = A.dims[0] + B.dims[0];
-    return dot3(d, d) < r * r;
+    return dot3(d, d) < r * r ? 1 : 0;
   }
   if ((A.kind == kSphere) != (B.kind == kSphere)) {
     const Shape<T>& S = A.kind == kSphere ? A : B;
@@ -223,34 +281,35 @@ IKG_HD inline bool pair_collides(const Shape<T>& A, const Shape<T>& B) {
         const T c = fmin(fmax(p[i], -X.dims[i]), X.dims[i]);
         e2 += (p[i] - c) * (p[i] - c);
       }
-      return e2 < S.dims[0] * S.dims[0];
+      return e2 < S.dims[0] * S.dims[0] ? 1 : 0;
     }
   }
-  return gjk_intersect(A, B);
+  return gjk_intersect(A, B, cert);
 }
 
 // ---------------------------------------------------------------- check stages
 // The stages of one check, shared by the wave-parallel driver (collide_wave,
 // ikg_collision.hip) and the host emulator.  Frames are [R(9) row-major, t(3)].
 
-// Joint-local transform placement * R_axis(q_j) (JointModelR*::calc).
+// Joint-local transform placement * R_axis(q_j) (JointModelR*::calc), given
+// (s, co) = sincos(q_j).
 template <typename T>
-IKG_HD inline void joint_local(const KModel<T>* __restrict__ m, int j, T qj, T* L) {
-  T s, co, R[9];
-  Prec<T>::sincos_(qj, &s, &co);
+IKG_HD inline void joint_local(const KModel<T>* __restrict__ m, int j, T s, T co, T* L) {
+  T R[9];
   for (int i = 0; i < 9; ++i) R[i] = m->jR[j][i];
   rotate_axis(R, m->jaxis[j], s, co);
   for (int i = 0; i < 9; ++i) L[i] = R[i];
   for (int i = 0; i < 3; ++i) L[9 + i] = m->jt[j][i];
 }
 
-// World frame of joint j (oMi): compose the local transforms up the parent chain.
+// World frame of joint j (oMi): compose the local transforms up the parent
+// chain (`par` = jparent, staged wherever the caller keeps it).
 template <typename T>
-IKG_HD inline void joint_world(const KModel<T>* __restrict__ m, int j, const T (*L)[12], T* F) {
+IKG_HD inline void joint_world(const int32_t* par, int j, const T (*L)[12], T* F) {
   T R[9], t[3];
   for (int i = 0; i < 9; ++i) R[i] = L[j][i];
   for (int i = 0; i < 3; ++i) t[i] = L[j][9 + i];
-  for (int k = m->jparent[j]; k >= 0; k = m->jparent[k]) {
+  for (int k = par[j]; k >= 0; k = par[k]) {
     T Rn[9], tn[3];
     matmul3(L[k], R, Rn);
     matvec3(L[k], t, tn);
@@ -281,16 +340,21 @@ IKG_HD inline void geom_world(const KCollision<T>* __restrict__ c, int g, const 
 
 // Pair k of the active list: bounding-sphere rejection, then the narrow phase.
 template <typename T>
-IKG_HD inline bool pair_hit(const KCollision<T>* __restrict__ c, int k, const T (*P)[12]) {
+IKG_HD inline int pair_hit(const KCollision<T>* __restrict__ c, int k, const T (*P)[12], T* cert = nullptr) {
   const int a = c->pairs[k][0], b = c->pairs[k][1];
   const T* Pa = P[a];
   const T* Pb = P[b];
   T d[3] = {Pa[9] - Pb[9], Pa[10] - Pb[10], Pa[11] - Pb[11]};
   const T r = c->brad[a] + c->brad[b];
-  if (dot3(d, d) >= r * r) return false;
+  if (dot3(d, d) >= r * r) return 0;
   const Shape<T> A{Pa, Pa + 9, c->dims[a], c->kind[a]};
   const Shape<T> B{Pb, Pb + 9, c->dims[b], c->kind[b]};
-  return pair_collides(A, B);
+  return pair_collides(A, B, cert);
+}
+
+template <typename T>
+IKG_HD inline Shape<T> pair_shape(const KCollision<T>* __restrict__ c, int g, const T (*P)[12]) {
+  return Shape<T>{P[g], P[g] + 9, c->dims[g], c->kind[g]};
 }
 
 }  // namespace ikg

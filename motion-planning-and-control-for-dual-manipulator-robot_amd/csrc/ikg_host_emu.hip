@@ -18,8 +18,12 @@ template <typename T>
 bool emu_collide(const ikg::KModel<T>& m, const ikg::KCollision<T>& c, const T* q, const T* tgt) {
   using namespace ikg;
   T L[kMaxNq][12], F[kMaxNq][12], P[kMaxGeoms][12];
-  for (int j = 0; j < m.nq; ++j) joint_local(&m, j, q[j], L[j]);
-  for (int j = 0; j < m.nq; ++j) joint_world(&m, j, L, F[j]);
+  for (int j = 0; j < m.nq; ++j) {
+    T s, co;
+    Prec<T>::sincos_(q[j], &s, &co);
+    joint_local(&m, j, s, co, L[j]);
+  }
+  for (int j = 0; j < m.nq; ++j) joint_world(m.jparent, j, L, F[j]);
   for (int g = 0; g < c.n_geoms; ++g) geom_world(&c, g, F, tgt, P[g]);
   for (int k = 0; k < c.n_pairs; ++k)
     if (pair_hit(&c, k, P)) return true;
