@@ -56,7 +56,7 @@ __device__ unsigned long long g_cprof[8];
 // wave-wide rounds of 64 with an early exit on the first round holding a hit,
 // whose lowest pair becomes the new witness.  The result is the OR over all
 // active pairs either way: only the order of the tests changes.
-template <typename T>
+template <typename T, bool WITNESS>
 __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
                              CollideScratch<T>& S, const T* tgt, Witness<T>& W,
                              unsigned long long* prof = nullptr) {
@@ -71,8 +71,8 @@ __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T
   __syncthreads();
   CPROF_MARK(a_fr, t);
   CPROF_ADD(0, a_fr);
-  const int w = W.pair;
-  if (w >= 0) {
+  const int w = WITNESS ? W.pair : -1;
+  if (WITNESS && w >= 0) {
     const int ga = c->pairs[w][0], gb = c->pairs[w][1];
     if (lane < 2) geom_world(c, lane ? gb : ga, S.F, tgt, S.P[lane ? gb : ga]);
     __syncthreads();
@@ -109,12 +109,12 @@ __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T
     const bool hit = k < c->n_pairs && k != w && pair_hit(c, k, S.P) != 0;
     const unsigned long long bal = __ballot(hit);
     if (bal) {
-      if (lane == 0) W.pair = base + __ffsll((long long)bal) - 1;
+      if (WITNESS && lane == 0) W.pair = base + __ffsll((long long)bal) - 1;
       found = true;
       break;
     }
   }
-  if (lane == 0) {
+  if (WITNESS && lane == 0) {
     if (!found) W.pair = -1;
     W.cert_ok = 0;
   }
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(64) void ikg_collision_kernel(const KModel<T>* __re
   __syncthreads();
   stage_trig_par(m, S);
   __syncthreads();
-  const bool col = collide_wave(m, c, S, tgt, W);
+  const bool col = collide_wave<T, false>(m, c, S, tgt, W);
   if (lane == 0) out[p] = col ? 1 : 0;
 }
 
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
     __syncthreads();
     CPROF_MARK(a_fk, t);
     if (it >= prm.max_iters) break;  // loop exhausted: success stays false
-    if (flag[0] != T(0) && !collide_wave(m, c, S, tgt, W, prof)) {
+    if (flag[0] != T(0) && !collide_wave<T, true>(m, c, S, tgt, W, prof)) {
       success = true;  // :70 errors pass and no collision
       break;
     }
