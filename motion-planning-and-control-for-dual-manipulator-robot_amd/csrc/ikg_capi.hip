@@ -227,7 +227,7 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, model->spec, s);
   if (e != hipSuccess) return hip_fail(e, "ikg pair kernel launch");
   if (dc) {
-    e = ikg::launch_collide_continue<T>(dm, dc, kparams<T>(params), a, model->spec, s);
+    e = ikg::launch_collide_continue<T>(dm, dc, kparams<T>(params), a, model->spec, nq, model->c64.n_geoms, s);
     if (e != hipSuccess) return hip_fail(e, "ikg collision continuation launch");
   }
   if (host) {
@@ -256,6 +256,7 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
     const ikg::KCollision<T>* dc = nullptr;
     if ((rc = model->collision_tables<T>(device, &dc))) return rc;
     a.collision = dc;
+    a.n_geoms = model->c64.n_geoms;
   }
   Staging st(s);
   const bool host = flags & IKG_FLAG_HOST_POINTERS;

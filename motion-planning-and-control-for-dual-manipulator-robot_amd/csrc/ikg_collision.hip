@@ -12,6 +12,8 @@
 //    ~745-pair check.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "ikg_collision.hpp"
 #include "ikg_device.hpp"
 #include "ikg_launch.hpp"
@@ -23,15 +25,16 @@ namespace ikg {
 // phase; totals are summed into g_cprof.
 #ifdef IKG_CPROF
 __device__ unsigned long long g_cprof[8];
-#define CPROF_MARK(acc, t)                      \
-  do {                                          \
-    const unsigned long long _n = clock64();    \
-    if ((threadIdx.x & 63) == 0) acc += _n - t; \
-    t = _n;                                     \
+// `cp_lead` (in scope at every use): this lane accumulates for its problem
+#define CPROF_MARK(acc, t)                   \
+  do {                                       \
+    const unsigned long long _n = clock64(); \
+    if (cp_lead) acc += _n - t;              \
+    t = _n;                                  \
   } while (0)
-#define CPROF_ADD(i, v)                             \
-  do {                                              \
-    if (prof && (threadIdx.x & 63) == 0) prof[i] += v; \
+#define CPROF_ADD(i, v)                 \
+  do {                                  \
+    if (prof && cp_lead) prof[i] += v; \
   } while (0)
 #else
 #define CPROF_MARK(acc, t) \
@@ -64,6 +67,7 @@ __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T
   const int nq = m->nq;
 #ifdef IKG_CPROF
   unsigned long long t = clock64(), a_fr = 0, a_w = 0, a_sw = 0;
+  const bool cp_lead = lane == 0;
 #endif
   if (lane < nq) joint_local(m, lane, S.sn[lane], S.cs[lane], S.L[lane]);
   __syncthreads();
@@ -155,78 +159,245 @@ __global__ __launch_bounds__(64) void ikg_collision_kernel(const KModel<T>* __re
   if (lane == 0) out[p] = col ? 1 : 0;
 }
 
-template <typename T, bool DAMPED, class SP>
+// ---------------------------------------------------------------- continuation
+// G problems per wave (LG = 64/G lanes each).  Per-problem state lives in a
+// slice of dynamic LDS sized for the model (group_lds_bytes).
+template <typename T>
+struct GroupLds {
+  T* q;
+  T* sn;
+  T* cs;
+  T (*F)[12];   // world joint frames of the current iterate
+  T (*L)[12];   // joint-local transforms of the passive joints (constant here)
+  T (*P)[12];   // geometry placements
+  T* tgt;
+  T* flag;
+  int32_t* par;
+  Witness<T>* W;
+};
+
+template <typename T>
+IKG_HD inline size_t group_lds_real_bytes(int nq, int ng) {
+  return (sizeof(T) * (27 * (size_t)nq + 12 * (size_t)ng + 16) + 15) & ~(size_t)15;
+}
+
+template <typename T>
+IKG_HD inline size_t group_lds_bytes(int nq, int ng) {
+  return group_lds_real_bytes<T>(nq, ng) + ((sizeof(int32_t) * (size_t)nq + 15) & ~(size_t)15) +
+         ((sizeof(Witness<T>) + 15) & ~(size_t)15);
+}
+
+template <typename T>
+__device__ inline GroupLds<T> group_view(char* base, int g, int nq, int ng) {
+  char* p = base + (size_t)g * group_lds_bytes<T>(nq, ng);
+  GroupLds<T> v;
+  T* t = (T*)p;
+  v.q = t;
+  t += nq;
+  v.sn = t;
+  t += nq;
+  v.cs = t;
+  t += nq;
+  v.F = (T(*)[12])t;
+  t += 12 * nq;
+  v.L = (T(*)[12])t;
+  t += 12 * nq;
+  v.P = (T(*)[12])t;
+  t += 12 * ng;
+  v.tgt = t;
+  t += 12;
+  v.flag = t;
+  char* c = p + group_lds_real_bytes<T>(nq, ng);
+  v.par = (int32_t*)c;
+  c += (sizeof(int32_t) * nq + 15) & ~(size_t)15;
+  v.W = (Witness<T>*)c;
+  return v;
+}
+
+// One collision check for every group with `need` set (group-uniform); all 64
+// lanes call it.  Joint frames come from the IK lanes' FK of the same iterate
+// (fk_arm WANT_FRAMES), so only the passive joints are composed here; then
+// witness-first / certificate / sweep exactly as collide_wave.  Returns the
+// group's verdict.
+template <typename T, int LG>
+__device__ bool collide_group(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
+                              const GroupLds<T>& V, int li, int lane0, bool need, unsigned long long gmask,
+                              unsigned long long* prof) {
+#ifdef IKG_CPROF
+  unsigned long long t = clock64(), a_fr = 0, a_w = 0, a_sw = 0;
+  const bool cp_lead = li == 0 && need;
+#endif
+  // root / arm joint frames were written by the IK lanes' FK of this iterate;
+  // the remaining (passive) joints hang off them, parents first (q order)
+  if (need && li == 0)
+    for (int i = 0; i < m->n_passive; ++i) {
+      const int j = m->passive_q[i];
+      const T* Lj = V.L[j];
+      const int a = V.par[j];
+      if (a < 0) {
+        for (int k = 0; k < 12; ++k) V.F[j][k] = Lj[k];
+      } else {
+        const T* Fp = V.F[a];
+        T tn[3];
+        matmul3(Fp, Lj, V.F[j]);
+        matvec3(Fp, Lj + 9, tn);
+        for (int k = 0; k < 3; ++k) V.F[j][9 + k] = Fp[9 + k] + tn[k];
+      }
+    }
+  __syncthreads();
+  const T(*Fa)[12] = V.F;
+  CPROF_MARK(a_fr, t);
+  CPROF_ADD(0, a_fr);
+  const int w = need ? V.W->pair : -1;
+  const bool has_w = w >= 0;
+  Witness<T>& W = *V.W;
+  if (has_w && li < 2) {  // the witness geometries' placements, from LDS only
+    T* P = W.P[li];
+    if (W.gtarget[li]) {
+      for (int i = 0; i < 12; ++i) P[i] = V.tgt[i];
+    } else if (W.gjoint[li] < 0) {
+      for (int i = 0; i < 9; ++i) P[i] = W.gR[li][i];
+      for (int i = 0; i < 3; ++i) P[9 + i] = W.gt[li][i];
+    } else {
+      const T* Fj = Fa[W.gjoint[li]];
+      T tn[3];
+      matmul3(Fj, W.gR[li], P);
+      matvec3(Fj, W.gt[li], tn);
+      for (int i = 0; i < 3; ++i) P[9 + i] = Fj[9 + i] + tn[i];
+    }
+  }
+  __syncthreads();
+  const Shape<T> A{W.P[0], W.P[0] + 9, W.gdims[0], W.gkind[0]};
+  const Shape<T> B{W.P[1], W.P[1] + 9, W.gdims[1], W.gkind[1]};
+  const bool cert = has_w && W.cert_ok;
+  if (cert && li < 4) mink_support(A, B, W.dir + 3 * li, W.pts[li]);
+  __syncthreads();
+  if (has_w && li == 0) {
+    int r = 0;
+    if (cert && tetra_encloses_origin(W.pts[0], W.pts[1], W.pts[2], W.pts[3])) {
+      r = 1;
+    } else {
+      T cd[12];
+      r = pair_collides(A, B, cd);
+      W.cert_ok = r == 2;
+      if (r == 2)
+        for (int i = 0; i < 12; ++i) W.dir[i] = cd[i];
+    }
+    V.flag[1] = r ? T(1) : T(0);
+  }
+  __syncthreads();
+  bool hit = has_w && V.flag[1] != T(0);
+  CPROF_MARK(a_w, t);
+  CPROF_ADD(1, a_w);
+  const bool sweep = need && !hit;
+  if (__any(sweep)) {
+    CPROF_ADD(3, sweep ? 1ull : 0ull);
+    if (sweep)
+      for (int g = li; g < c->n_geoms; g += LG) geom_world(c, g, Fa, V.tgt, V.P[g]);
+    __syncthreads();
+    bool done = !sweep, found = false;
+    int wnew = -1;
+    for (int base = 0;; base += LG) {
+      const int k = base + li;
+      const bool h = !done && k < c->n_pairs && k != w && pair_hit(c, k, V.P) != 0;
+      const unsigned long long bal = __ballot(h) & gmask;
+      if (!done && bal) {
+        found = true;
+        wnew = base + (__ffsll((long long)bal) - 1 - lane0);
+      }
+      done = done || bal != 0 || base + LG >= c->n_pairs;
+      if (!__any(!done)) break;
+    }
+    if (sweep && li == 0) {
+      W.pair = wnew;
+      W.cert_ok = 0;
+    }
+    if (sweep && found && li < 2) {  // cache the new witness's geometry constants
+      const int g = c->pairs[wnew][li];
+      W.gjoint[li] = c->joint[g];
+      W.gkind[li] = c->kind[g];
+      W.gtarget[li] = g == c->target_geom;
+      for (int i = 0; i < 9; ++i) W.gR[li][i] = c->R[g][i];
+      for (int i = 0; i < 3; ++i) W.gt[li][i] = c->t[g][i];
+      for (int i = 0; i < 3; ++i) W.gdims[li][i] = c->dims[g][i];
+    }
+    if (sweep) hit = found;
+    CPROF_MARK(a_sw, t);
+    CPROF_ADD(2, a_sw);
+  }
+  return hit;
+}
+
+template <typename T, bool DAMPED, class SP, int G>
 __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T>* __restrict__ m,
                                                                   const KCollision<T>* __restrict__ c,
                                                                   KParams<T> prm, const T* __restrict__ targets,
-                                                                  int64_t S_per_target, T* __restrict__ q_out,
+                                                                  int64_t S_per_target, int64_t B,
+                                                                  T* __restrict__ q_out,
                                                                   uint8_t* __restrict__ conv,
                                                                   int32_t* __restrict__ iters,
                                                                   T* __restrict__ err) {
-  __shared__ CollideScratch<T> S;
-  __shared__ T tgt[12];
-  __shared__ T flag[4];
-  __shared__ Witness<T> W;
-  const int64_t p = blockIdx.x;
+  extern __shared__ __align__(16) char lds[];
+  constexpr int LG = 64 / G;
   const int lane = threadIdx.x;
-  if (!conv[p]) return;  // only problems whose hand errors passed (uniform per workgroup)
+  const int g = lane / LG, li = lane % LG, lane0 = g * LG;
+  const unsigned long long gmask = LG == 64 ? ~0ull : (((1ull << LG) - 1ull) << lane0);
   const int nq = m->nq;
-  const int64_t t_idx = S_per_target > 1 ? p / S_per_target : p;
-  if (lane < nq) S.q[lane] = q_out[p * nq + lane];
-  if (lane < 12) tgt[lane] = targets[t_idx * 12 + lane];
-  if (lane == 0) {
-    W.pair = -1;
-    W.cert_ok = 0;
+  const GroupLds<T> V = group_view<T>(lds, g, nq, c->n_geoms);
+  const int64_t p = (int64_t)blockIdx.x * G + g;
+  // problems whose hand errors passed in the pair kernel (group-uniform)
+  const bool started = p < B && conv[p] != 0;
+  if (!__any(started)) return;  // whole wave
+  bool active = started;
+  if (active) {
+    const int64_t t_idx = S_per_target > 1 ? p / S_per_target : p;
+    for (int j = li; j < nq; j += LG) {
+      const T qj = q_out[p * nq + j];
+      V.q[j] = qj;
+      Prec<T>::sincos_(qj, &V.sn[j], &V.cs[j]);
+      joint_local(m, j, V.sn[j], V.cs[j], V.L[j]);  // the passive joints' entries are used
+      V.par[j] = m->jparent[j];
+    }
+    if (li < 12) V.tgt[li] = targets[t_idx * 12 + li];
+    if (li == 0) {
+      V.W->pair = -1;
+      V.W->cert_ok = 0;
+    }
   }
   __syncthreads();
-  stage_trig_par(m, S);  // passive joints keep these; lanes 0/1 refresh the rest
-  const int arm = lane & 1;
-  const bool pair_lane = lane < 2;
-  T RT[9], tT[3], qc = T(0), qa[kArmDof] = {};
-  if (pair_lane) {
-    hook_target(m, arm, tgt, RT, tT);
-    qc = S.q[m->root_q];
-    for (int k = 0; k < kArmDof; ++k) qa[k] = S.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]];
+  const int arm = li & 1;
+  const bool ik = active && li < 2;
+  T RT[9], tT[3], qc = T(0), qa[kArmDof] = {}, sn[7], cs[7];
+  if (ik) {
+    hook_target(m, arm, V.tgt, RT, tT);
+    qc = V.q[m->root_q];
+    for (int k = 0; k < kArmDof; ++k) qa[k] = V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]];
+    trig_exact(qc, qa, sn, cs);
   }
-  int it = iters[p];
-  bool success = false;
-  T nrm = T(0), other = T(0);
+  int it = active ? iters[p] : 0;
+  bool success = false, passive_clamped = it > 0;
+  T nrm = T(0);
 #ifdef IKG_CPROF
   unsigned long long prof[4] = {0, 0, 0, 0}, t = clock64(), a_fk = 0, a_up = 0, a_col = 0;
   const int it0 = it;
+  bool cp_lead = li == 0 && active;
 #else
   unsigned long long* prof = nullptr;
 #endif
-  bool passive_clamped = it > 0;
   for (;;) {
-    __syncthreads();  // stage_trig_par / the previous update wrote S
-    ArmState<T> st;
-    if (pair_lane) {  // hand errors at the current iterate (:58-67)
-      T sn[7], cs[7];
-      trig_exact(qc, qa, sn, cs);
-      nrm = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
-      other = pair_swap(nrm);
-      if (lane == 0) {
-        flag[0] = (nrm < prm.eps && other < prm.eps) ? T(1) : T(0);
-        S.sn[m->root_q] = sn[0];
-        S.cs[m->root_q] = cs[0];
-      }
-      for (int k = 0; k < kArmDof; ++k) {
-        const int j = arm ? m->arm_q[1][k] : m->arm_q[0][k];
-        S.sn[j] = sn[k + 1];
-        S.cs[j] = cs[k + 1];
-      }
-    }
-    __syncthreads();
-    CPROF_MARK(a_fk, t);
-    if (it >= prm.max_iters) break;  // loop exhausted: success stays false
-    if (flag[0] != T(0) && !collide_wave<T, true>(m, c, S, tgt, W, prof)) {
-      success = true;  // :70 errors pass and no collision
-      break;
-    }
-    CPROF_MARK(a_col, t);
-    if (pair_lane) {  // one update (:75-89)
-      T dq[6], alpha, beta, s;
+#ifdef IKG_CPROF
+    cp_lead = li == 0 && active;
+#endif
+    // FK + errors at the current iterate (:58-67) and, before the collision
+    // check, the update it would take (:75-83): the Jacobian state dies here,
+    // so only q, dq and the trig state stay live across the check
+    T dq[6], s = T(0);
+    if (active && li < 2) {
+      ArmState<T> st;
+      nrm = arm_fk_error<T, SP, true>(m, arm, sn, cs, RT, tT, st, V.F);
+      const T other = pair_swap(nrm);
+      if (li == 0) V.flag[0] = (nrm < prm.eps && other < prm.eps) ? T(1) : T(0);
+      T alpha, beta;
       if constexpr (!DAMPED) {
         T u[6], v[6];
         arm_solve<T, SP>(st, u, v, alpha, beta);
@@ -239,27 +410,47 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
         s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
         arm_dq_damped(A, ze, zc, s, dq);
       }
-      arm_update(m, arm, prm.dt, s, dq, qc, qa);
     }
-    __syncthreads();  // the collision check may still be reading S.q
-    if (pair_lane) {
-      if (arm == 0) S.q[m->root_q] = qc;
-      for (int k = 0; k < kArmDof; ++k) S.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
-    }
-    if (!passive_clamped) {  // projecttojointlimits on every joint after the first update
-      for (int i = lane; i < m->n_passive; i += 64) {
-        const int j = m->passive_q[i];
-        S.q[j] = clampq(S.q[j], m->lo[j], m->hi[j]);
-        Prec<T>::sincos_(S.q[j], &S.sn[j], &S.cs[j]);
+    __syncthreads();
+    CPROF_MARK(a_fk, t);
+    if (active && it >= prm.max_iters) active = false;  // loop exhausted: success stays false
+    const bool need = active && V.flag[0] != T(0);
+    if (__any(need)) {
+      const bool col = collide_group<T, LG>(m, c, V, li, lane0, need, gmask, prof);
+      if (need && !col) {
+        success = true;  // :70 errors pass and no collision
+        active = false;
       }
-      passive_clamped = true;
     }
-    ++it;
+    CPROF_MARK(a_col, t);
+    if (active && li < 2) {  // apply the update (:86-89)
+      T q_old[7];
+      q_old[0] = qc;
+      for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
+      arm_update(m, arm, prm.dt, s, dq, qc, qa);
+      trig_advance(qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);
+      if (arm == 0) V.q[m->root_q] = qc;
+      for (int k = 0; k < kArmDof; ++k) V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
+    }
+    if (active && !passive_clamped) {  // projecttojointlimits on every joint after the first update
+      for (int i = li; i < m->n_passive; i += LG) {
+        const int j = m->passive_q[i];
+        V.q[j] = clampq(V.q[j], m->lo[j], m->hi[j]);
+        Prec<T>::sincos_(V.q[j], &V.sn[j], &V.cs[j]);
+        joint_local(m, j, V.sn[j], V.cs[j], V.L[j]);
+      }
+    }
+    if (active) {
+      passive_clamped = true;
+      ++it;
+    }
     CPROF_MARK(a_up, t);
+    if (!__any(active)) break;
+    __syncthreads();
   }
   __syncthreads();
 #ifdef IKG_CPROF
-  if (lane == 0) {
+  if (li == 0 && started) {
     atomicAdd(&g_cprof[0], a_fk);
     atomicAdd(&g_cprof[1], a_col);
     atomicAdd(&g_cprof[2], a_up);
@@ -270,10 +461,10 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
     atomicAdd(&g_cprof[7], (unsigned long long)(it - it0));
   }
 #endif
-  if (lane < nq) q_out[p * nq + lane] = S.q[lane];
-  if (pair_lane) {
-    err[p * 2 + arm] = nrm;
-    if (lane == 0) {
+  if (started) {
+    for (int j = li; j < nq; j += LG) q_out[p * nq + j] = V.q[j];
+    if (li < 2) err[p * 2 + arm] = nrm;
+    if (li == 0) {
       conv[p] = success ? 1 : 0;
       iters[p] = it;
     }
@@ -290,28 +481,49 @@ hipError_t launch_collision(const KModel<T>* dm, const KCollision<T>* dc, const 
   return hipGetLastError();
 }
 
+// problems per continuation wave (IKG_CONT_G=1 selects one per wave; timing knob)
+static int cont_groups() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("IKG_CONT_G");
+    v = (e && atoi(e) == 1) ? 1 : 4;
+  }
+  return v;
+}
+
+template <typename T, bool DAMPED, class SP, int G>
+static void launch_continue_g(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
+                              const BatchArgs& a, int nq, int ng, hipStream_t s) {
+  const size_t lds = (size_t)G * group_lds_bytes<T>(nq, ng);
+  hipLaunchKernelGGL((ikg_collide_continue_kernel<T, DAMPED, SP, G>), dim3((unsigned)((a.B + G - 1) / G)), dim3(64),
+                     lds, s, dm, dc, prm, (const T*)a.targets, a.S, a.B, (T*)a.q_out, a.converged, a.iters,
+                     (T*)a.err_out);
+}
+
 template <typename T, bool DAMPED, class SP>
 static void launch_continue_t(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
-                              const BatchArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((ikg_collide_continue_kernel<T, DAMPED, SP>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, prm,
-                     (const T*)a.targets, a.S, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out);
+                              const BatchArgs& a, int nq, int ng, hipStream_t s) {
+  if (cont_groups() == 1)
+    launch_continue_g<T, DAMPED, SP, 1>(dm, dc, prm, a, nq, ng, s);
+  else
+    launch_continue_g<T, DAMPED, SP, 4>(dm, dc, prm, a, nq, ng, s);
 }
 
 template <typename T>
 hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
-                                   const BatchArgs& a, int spec, hipStream_t s) {
+                                   const BatchArgs& a, int spec, int nq, int ng, hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
   const bool damped = prm.lambda > T(0);
   if (spec == kSpecNextage) {
     if (damped)
-      launch_continue_t<T, true, SpecNextage>(dm, dc, prm, a, s);
+      launch_continue_t<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, s);
     else
-      launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, s);
+      launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, nq, ng, s);
   } else {
     if (damped)
-      launch_continue_t<T, true, SpecGeneric>(dm, dc, prm, a, s);
+      launch_continue_t<T, true, SpecGeneric>(dm, dc, prm, a, nq, ng, s);
     else
-      launch_continue_t<T, false, SpecGeneric>(dm, dc, prm, a, s);
+      launch_continue_t<T, false, SpecGeneric>(dm, dc, prm, a, nq, ng, s);
   }
   return hipGetLastError();
 }
@@ -332,8 +544,10 @@ template hipError_t launch_collision<double>(const KModel<double>*, const KColli
 template hipError_t launch_collision<float>(const KModel<float>*, const KCollision<float>*, const void*,
                                             const void*, int64_t, uint8_t*, hipStream_t);
 template hipError_t launch_collide_continue<double>(const KModel<double>*, const KCollision<double>*,
-                                                    const KParams<double>&, const BatchArgs&, int, hipStream_t);
+                                                    const KParams<double>&, const BatchArgs&, int, int, int,
+                                                    hipStream_t);
 template hipError_t launch_collide_continue<float>(const KModel<float>*, const KCollision<float>*,
-                                                   const KParams<float>&, const BatchArgs&, int, hipStream_t);
+                                                   const KParams<float>&, const BatchArgs&, int, int, int,
+                                                   hipStream_t);
 
 }  // namespace ikg

@@ -54,6 +54,14 @@ struct Witness {
   int32_t cert_ok;  // dir[] valid
   T dir[12];
   T pts[4][3];
+  // the pair's two geometries, cached when the witness is set (continuation)
+  int32_t gjoint[2];
+  int32_t gkind[2];
+  int32_t gtarget[2];
+  T gR[2][9];
+  T gt[2][3];
+  T gdims[2][3];
+  T P[2][12];  // their world placements at the current iterate
 };
 
 template <typename T>

@@ -360,9 +360,11 @@ IKG_HD inline void column_ax(const T* R, int runtime_axis, T* a) {
 // (sin, cos) (slot 0 = root, 1..6 = arm), producing
 //   Rh, th  : effector frame placement oMf (data.oMf[LARM/RARM_EFF], :62-63)
 //   ax, org : world axis / origin of the 7 supporting joints (root first)
-template <typename T, class SP, bool WANT_AXES>
+//   frames  : (WANT_FRAMES) world frame [R|t] of every supporting joint, stored
+//             at its q index (the root only by the left lane); collision check
+template <typename T, class SP, bool WANT_AXES, bool WANT_FRAMES = false>
 IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, T* Rh, T* th,
-                          T (*ax)[3], T (*org)[3]) {
+                          T (*ax)[3], T (*org)[3], T (*frames)[12] = nullptr) {
   T R[9], t[3];
   if constexpr (SP::prot) {
 #pragma unroll
@@ -380,6 +382,15 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* sn,
     for (int i = 0; i < 3; ++i) org[0][i] = t[i];
   }
   const bool right = arm != 0;
+  if constexpr (WANT_FRAMES) {
+    if (!right) {
+      T* F = frames[m->root_q];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) F[i] = R[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) F[9 + i] = t[i];
+    }
+  }
 #pragma unroll
   for (int k = 0; k < kArmDof; ++k) {
     T pt[3], dt_[3];
@@ -417,6 +428,13 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* sn,
       }
 #pragma unroll
       for (int i = 0; i < 3; ++i) org[k + 1][i] = t[i];
+    }
+    if constexpr (WANT_FRAMES) {
+      T* F = frames[right ? m->arm_q[1][k] : m->arm_q[0][k]];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) F[i] = R[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) F[9 + i] = t[i];
     }
   }
   T ht[3], d[3];
@@ -592,10 +610,10 @@ IKG_HD inline void trig_advance(T qc, const T* qa, const T* q_old, bool resync, 
 }
 
 // FK + pose error; returns |e| (inverse_geometry.py:58-67).
-template <typename T, class SP>
+template <typename T, class SP, bool WANT_FRAMES = false>
 IKG_HD inline T arm_fk_error(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, const T* RT,
-                             const T* tT, ArmState<T>& st) {
-  fk_arm<T, SP, true>(m, arm, sn, cs, st.Rh, st.th, st.ax, st.org);
+                             const T* tT, ArmState<T>& st, T (*frames)[12] = nullptr) {
+  fk_arm<T, SP, true, WANT_FRAMES>(m, arm, sn, cs, st.Rh, st.th, st.ax, st.org, frames);
   pose_error(st.Rh, st.th, RT, tT, st.e);
   const T* e = st.e;
   return sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3] + e[4] * e[4] + e[5] * e[5]);

@@ -300,7 +300,7 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   hipError_t e = launch_pair_batch<T>(dmodel, prm, b, spec, s);
   if (e != hipSuccess) return e;
   if (a.collision) {  // converged-but-colliding seeds keep iterating (inverse_geometry.py:70)
-    e = launch_collide_continue<T>(dmodel, (const KCollision<T>*)a.collision, prm, b, spec, s);
+    e = launch_collide_continue<T>(dmodel, (const KCollision<T>*)a.collision, prm, b, spec, a.nq, a.n_geoms, s);
     if (e != hipSuccess) return e;
   }
   // 2) one wave per target picks the best seed

@@ -41,6 +41,7 @@ struct MultiArgs {
   // KCollision<T>* (device) when params.check_collision: the seeds' results
   // go through the collision continuation before the best-seed reduction
   const void* collision = nullptr;
+  int n_geoms = 0;
 };
 
 // kernel specialisation chosen at model creation (ikg_model_build.hpp)
@@ -70,8 +71,9 @@ template <typename T>
 hipError_t launch_collision(const KModel<T>* dm, const KCollision<T>* dc, const void* q, const void* targets,
                             int64_t B, uint8_t* out, hipStream_t s);
 
+// nq / ng: model joints and scene geometries (size the per-problem LDS slices)
 template <typename T>
 hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
-                                   const BatchArgs& a, int spec, hipStream_t s);
+                                   const BatchArgs& a, int spec, int nq, int ng, hipStream_t s);
 
 }  // namespace ikg
