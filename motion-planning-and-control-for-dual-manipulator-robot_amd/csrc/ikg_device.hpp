@@ -54,6 +54,8 @@ struct KModel {
   T hand_sc[2][2];    // (sin, cos) of that angle per hand
   int32_t wrist;      // 1: axes of arm joints 3,4,5 meet at the origin of arm joint 4
   int32_t pattern;    // compile-time specialisation code (ikg_model_build.hpp)
+  int32_t zmask;      // bit 3k+i: arm_t[*][k][i] == 0 for both arms (k < 6)
+  T hand_tH[2][3];    // hand_R^T hand_t: hand offset seen from the hand frame
   // full kinematic tree (every joint, q order) for the collision check
   T jR[kMaxNq][9];
   T jt[kMaxNq][3];
@@ -67,17 +69,26 @@ struct KModel {
 constexpr int kAxRuntime = 3;
 constexpr int kPatternGeneric = 0xFFFF;
 
-template <int PAT, bool PROT, bool WRIST>
+template <int PAT, bool PROT, bool WRIST, int ZMASK = 0>
 struct Spec {
   static constexpr int axis(int slot) { return (PAT >> (2 * slot)) & 3; }
   static constexpr bool prot = PROT;    // arm joint placements carry rotations
   static constexpr bool wrist = WRIST;  // decoupled spherical-wrist solve
+  // arm joint k's placement offset component i is exactly 0 (both arms)
+  static constexpr bool zero_t(int k, int i) { return (ZMASK >> (3 * k + i)) & 1; }
+  static constexpr int zmask = ZMASK;
+  // the hand frame rotation turns about the last arm joint's axis: fold it
+  // into that joint's angle (Rh = R5 Rot(q5 + hand angle))
+  static constexpr bool fold_hand = axis(7) != kAxRuntime && axis(7) == axis(6);
 };
 using SpecGeneric = Spec<kPatternGeneric, true, false>;
 // Nextage (NextageaOpen.urdf:580-730): root Z; arm Z,Y,Y,X,Y,Z; hand Rz(1.5708);
 // identity joint placements; spherical wrist at LARM/RARM_JOINT4.
 constexpr int kPatternNextage = 2 | (2 << 2) | (1 << 4) | (1 << 6) | (0 << 8) | (1 << 10) | (2 << 12) | (2 << 14);
-using SpecNextage = Spec<kPatternNextage, false, true>;
+// zero offset components of the arm joint placements (URDF :580-730, both arms):
+// J1 (0,0,z)  J2 (0,y,z)  J3 (x,0,z)  J4 (x,0,0)  J5 (0,0,z)
+constexpr int kZeroNextage = (3 << 3) | (1 << 6) | (2 << 9) | (6 << 12) | (3 << 15);
+using SpecNextage = Spec<kPatternNextage, false, true, kZeroNextage>;
 
 template <typename T>
 struct KParams {
@@ -174,6 +185,16 @@ IKG_HD inline void matmul3_tn(const T* A, const T* B, T* C) {
 #pragma unroll
     for (int c = 0; c < 3; ++c)
       C[3 * r + c] = A[0 + r] * B[0 + c] + A[3 + r] * B[3 + c] + A[6 + r] * B[6 + c];
+}
+
+// C = A B^T
+template <typename T>
+IKG_HD inline void matmul3_nt(const T* A, const T* B, T* C) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+      C[3 * r + c] = A[3 * r + 0] * B[3 * c + 0] + A[3 * r + 1] * B[3 * c + 1] + A[3 * r + 2] * B[3 * c + 2];
 }
 
 template <typename T>
@@ -355,27 +376,42 @@ IKG_HD inline void column_ax(const T* R, int runtime_axis, T* a) {
     column(R, AX, a);
 }
 
-// Forward kinematics of the shared root joint + one arm (pin.forwardKinematics
-// restricted to the hand's support, inverse_geometry.py:58) given the joints'
-// (sin, cos) (slot 0 = root, 1..6 = arm), producing
-//   Rh, th  : effector frame placement oMf (data.oMf[LARM/RARM_EFF], :62-63)
-//   ax, org : world axis / origin of the 7 supporting joints (root first)
-//   frames  : (WANT_FRAMES) world frame [R|t] of every supporting joint, stored
-//             at its q index (the root only by the left lane); collision check
-template <typename T, class SP, bool WANT_AXES, bool WANT_FRAMES = false>
-IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, T* Rh, T* th,
-                          T (*ax)[3], T (*org)[3], T (*frames)[12] = nullptr) {
-  T R[9], t[3];
+// Frame of the shared root joint after its rotation: Rc = root_R Rot(q_root),
+// tc = root_t (the "chest frame"; setup_pinocchio.py:32 folds ROBOT_PLACEMENT
+// into root_t).
+template <typename T, class SP>
+IKG_HD inline void root_frame(const KModel<T>* __restrict__ m, T s0, T c0, T* Rc, T* tc) {
   if constexpr (SP::prot) {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) R[i] = m->root_R[i];
+    for (int i = 0; i < 9; ++i) Rc[i] = m->root_R[i];
   } else {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? T(1) : T(0);
+    for (int i = 0; i < 9; ++i) Rc[i] = (i % 4 == 0) ? T(1) : T(0);
   }
 #pragma unroll
-  for (int i = 0; i < 3; ++i) t[i] = m->root_t[i];
-  rotate_ax<SP::axis(0)>(R, m->root_axis, sn[0], cs[0]);
+  for (int i = 0; i < 3; ++i) tc[i] = m->root_t[i];
+  rotate_ax<SP::axis(0)>(Rc, m->root_axis, s0, c0);
+}
+
+// Forward kinematics of one arm (pin.forwardKinematics restricted to the
+// hand's support, inverse_geometry.py:58) from the root frame (R0, t0) given
+// the arm joints' (sin, cos) (slots 1..6; slot 0 = root, already in R0),
+// producing
+//   Rh, th  : effector frame placement (data.oMf[LARM/RARM_EFF], :62-63)
+//   ax, org : axis / origin of the 7 supporting joints (root first)
+//   frames  : (WANT_FRAMES) frame [R|t] of every supporting joint, stored at
+//             its q index (the root only by the left lane); collision check
+// in the coordinates of (R0, t0).  With (R0, t0) = (I, 0) everything is in the
+// chest frame: the root rotation and the arm's zero placement components fold
+// away at compile time (Spec).
+template <typename T, class SP, bool WANT_AXES, bool WANT_FRAMES = false>
+IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0, const T* t0, const T* sn,
+                          const T* cs, T* Rh, T* th, T (*ax)[3], T (*org)[3], T (*frames)[12] = nullptr) {
+  T R[9], t[3];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = R0[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = t0[i];
   if constexpr (WANT_AXES) {
     column_ax<SP::axis(0)>(R, m->root_axis, ax[0]);
 #pragma unroll
@@ -391,11 +427,14 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* sn,
       for (int i = 0; i < 3; ++i) F[9 + i] = t[i];
     }
   }
+  // hand rotation folded into the last joint's angle (not when the joint's own
+  // frame is wanted)
+  constexpr bool FOLD = SP::fold_hand && !WANT_FRAMES;
 #pragma unroll
   for (int k = 0; k < kArmDof; ++k) {
     T pt[3], dt_[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) pt[i] = sel(right, m->arm_t[1][k][i], m->arm_t[0][k][i]);
+    for (int i = 0; i < 3; ++i) pt[i] = SP::zero_t(k, i) ? T(0) : sel(right, m->arm_t[1][k][i], m->arm_t[0][k][i]);
     matvec3(R, pt, dt_);
 #pragma unroll
     for (int i = 0; i < 3; ++i) t[i] += dt_[i];
@@ -415,9 +454,18 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* sn,
       case 2: rotate_ax<SP::axis(3)>(R, m->arm_axis[2], sn[3], cs[3]); break;
       case 3: rotate_ax<SP::axis(4)>(R, m->arm_axis[3], sn[4], cs[4]); break;
       case 4: rotate_ax<SP::axis(5)>(R, m->arm_axis[4], sn[5], cs[5]); break;
-      default: rotate_ax<SP::axis(6)>(R, m->arm_axis[5], sn[6], cs[6]); break;
+      default:
+        if constexpr (FOLD) {
+          // Rot(q5) Rot(h) = Rot(q5 + h): (sin, cos) by angle addition
+          const T hs = sel(right, m->hand_sc[1][0], m->hand_sc[0][0]);
+          const T hc = sel(right, m->hand_sc[1][1], m->hand_sc[0][1]);
+          rotate_axis(R, SP::axis(6), sn[6] * hc + cs[6] * hs, cs[6] * hc - sn[6] * hs);
+        } else {
+          rotate_ax<SP::axis(6)>(R, m->arm_axis[5], sn[6], cs[6]);
+        }
+        break;
     }
-    if constexpr (WANT_AXES) {
+    if constexpr (WANT_AXES) {  // a rotation about an axis leaves that column unchanged (FOLD)
       switch (k) {
         case 0: column_ax<SP::axis(1)>(R, m->arm_axis[0], ax[1]); break;
         case 1: column_ax<SP::axis(2)>(R, m->arm_axis[1], ax[2]); break;
@@ -438,24 +486,43 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* sn,
     }
   }
   T ht[3], d[3];
+  if constexpr (FOLD) {
+    // R is already the hand rotation: th = t + R6 ht = t + Rh (hand_R^T ht)
 #pragma unroll
-  for (int i = 0; i < 3; ++i) ht[i] = sel(right, m->hand_t[1][i], m->hand_t[0][i]);
-  matvec3(R, ht, d);
+    for (int i = 0; i < 3; ++i) ht[i] = sel(right, m->hand_tH[1][i], m->hand_tH[0][i]);
+    matvec3(R, ht, d);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) th[i] = t[i] + d[i];
-  constexpr int HA = SP::axis(7);
-  if constexpr (HA != kAxRuntime) {
-    // hand placement rotation = R_axis(angle): two columns change
+    for (int i = 0; i < 3; ++i) th[i] = t[i] + d[i];
 #pragma unroll
     for (int i = 0; i < 9; ++i) Rh[i] = R[i];
-    rotate_axis(Rh, HA, sel(right, m->hand_sc[1][0], m->hand_sc[0][0]),
-                sel(right, m->hand_sc[1][1], m->hand_sc[0][1]));
   } else {
-    T hR[9];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) hR[i] = sel(right, m->hand_R[1][i], m->hand_R[0][i]);
-    matmul3(R, hR, Rh);
+    for (int i = 0; i < 3; ++i) ht[i] = sel(right, m->hand_t[1][i], m->hand_t[0][i]);
+    matvec3(R, ht, d);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) th[i] = t[i] + d[i];
+    constexpr int HA = SP::axis(7);
+    if constexpr (HA != kAxRuntime) {
+      // hand placement rotation = R_axis(angle): two columns change
+#pragma unroll
+      for (int i = 0; i < 9; ++i) Rh[i] = R[i];
+      rotate_axis(Rh, HA, sel(right, m->hand_sc[1][0], m->hand_sc[0][0]),
+                  sel(right, m->hand_sc[1][1], m->hand_sc[0][1]));
+    } else {
+      T hR[9];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) hR[i] = sel(right, m->hand_R[1][i], m->hand_R[0][i]);
+      matmul3(R, hR, Rh);
+    }
   }
+}
+
+// World-frame FK of one arm (batch FK kernel, diagnostics).
+template <typename T, class SP>
+IKG_HD inline void fk_arm_world(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, T* Rh, T* th) {
+  T Rc[9], tc[3];
+  root_frame<T, SP>(m, sn[0], cs[0], Rc, tc);
+  fk_arm<T, SP, false>(m, arm, Rc, tc, sn, cs, Rh, th, nullptr, nullptr);
 }
 
 // log6(oMhand^-1 * oMtarget) (inverse_geometry.py:66-67)
@@ -471,6 +538,25 @@ IKG_HD inline void pose_error(const T* Rh, const T* th, const T* RT, const T* tT
     e[3] = T(0.5) * (Rm[7] - Rm[5]); e[4] = T(0.5) * (Rm[2] - Rm[6]); e[5] = T(0.5) * (Rm[3] - Rm[1]);
   } else {
     log6(Rm, pm, e);
+  }
+}
+
+// The same error expressed in the axes of the frame (Rh, th) is given in:
+// with Rw = RT Rh^T = Rh Rm Rh^T and d = tT - th = Rh pm, log3(Rw) = Rh log3(Rm)
+// and V(w)^-1 commutes with the rotation, so log6(Rw, d) = blockdiag(Rh, Rh)
+// log6(Rm, pm): the reference's LOCAL error rotated into the frame's axes (same
+// norm, same minimum-norm step).
+template <typename T>
+IKG_HD inline void pose_error_aligned(const T* Rh, const T* th, const T* RT, const T* tT, T* e) {
+  T Rw[9], d[3];
+  matmul3_nt(RT, Rh, Rw);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) d[i] = tT[i] - th[i];
+  if constexpr (IKG_ABL & 2) {
+    e[0] = d[0]; e[1] = d[1]; e[2] = d[2];
+    e[3] = T(0.5) * (Rw[7] - Rw[5]); e[4] = T(0.5) * (Rw[2] - Rw[6]); e[5] = T(0.5) * (Rw[3] - Rw[1]);
+  } else {
+    log6(Rw, d, e);
   }
 }
 
@@ -577,9 +663,9 @@ IKG_HD inline T clampq(T q, T lo, T hi) {
 // on the CPU.
 template <typename T>
 struct ArmState {
-  T Rh[9], th[3];         // effector placement oMf
-  T ax[7][3], org[7][3];  // world axis / origin of root + arm joints
-  T e[6];                 // log6(oMf^-1 oMtarget)
+  T Rh[9], th[3];         // effector placement, in the iteration's frame (below)
+  T ax[7][3], org[7][3];  // axis / origin of root + arm joints, same frame
+  T e[6];                 // log6(oMf^-1 oMtarget) rotated into that frame's axes
 };
 
 // exact (sin, cos) of the root and arm joints (slot 0 = root)
@@ -609,19 +695,38 @@ IKG_HD inline void trig_advance(T qc, const T* qa, const T* q_old, bool resync, 
   }
 }
 
-// FK + pose error; returns |e| (inverse_geometry.py:58-67).
-template <typename T, class SP, bool WANT_FRAMES = false>
+// FK + pose error; returns |e| (inverse_geometry.py:58-67).  WORLD = false
+// (the IK loop): everything in the chest frame (root_frame) -- the target is
+// moved into it (Rc^T RT, Rc^T (tT - tc)) instead of the arm's 7 frames out of
+// it.  WORLD = true: world frame (collision continuation, which needs world
+// joint frames).  The minimum-norm step is the same in any frame (§3).
+template <typename T, class SP, bool WANT_FRAMES = false, bool WORLD = WANT_FRAMES>
 IKG_HD inline T arm_fk_error(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, const T* RT,
                              const T* tT, ArmState<T>& st, T (*frames)[12] = nullptr) {
-  fk_arm<T, SP, true, WANT_FRAMES>(m, arm, sn, cs, st.Rh, st.th, st.ax, st.org, frames);
-  pose_error(st.Rh, st.th, RT, tT, st.e);
+  T Rc[9], tc[3];
+  root_frame<T, SP>(m, sn[0], cs[0], Rc, tc);
+  if constexpr (WORLD) {
+    fk_arm<T, SP, true, WANT_FRAMES>(m, arm, Rc, tc, sn, cs, st.Rh, st.th, st.ax, st.org, frames);
+    pose_error_aligned(st.Rh, st.th, RT, tT, st.e);
+  } else {
+    static_assert(!WANT_FRAMES, "joint frames are produced in the world frame");
+    const T I3[9] = {T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)};
+    const T Z3[3] = {T(0), T(0), T(0)};
+    fk_arm<T, SP, true>(m, arm, I3, Z3, sn, cs, st.Rh, st.th, st.ax, st.org);
+    T RTc[9], dT[3], tTc[3];
+    matmul3_tn(Rc, RT, RTc);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dT[i] = tT[i] - tc[i];
+    matvec3_t(Rc, dT, tTc);
+    pose_error_aligned(st.Rh, st.th, RTc, tTc, st.e);
+  }
   const T* e = st.e;
   return sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3] + e[4] * e[4] + e[5] * e[5]);
 }
 
-// World-aligned Jacobian at the hand point, col_j = [a_j x (p_h - o_j); a_j]
-// (columns 0..5 = arm joints, 7 = root) and the rotated error Rh e (column 6).
-// LOCAL = blockdiag(Rh^T, Rh^T) * world-aligned (:75-76), and the rotation is
+// Frame-aligned Jacobian at the hand point, col_j = [a_j x (p_h - o_j); a_j]
+// (columns 0..5 = arm joints, 7 = root) and the aligned error (column 6).
+// LOCAL = blockdiag(Rh^T, Rh^T) * aligned (:75-76), and the rotation is
 // orthogonal, so the minimum-norm step is unchanged.
 template <typename T>
 IKG_HD inline void arm_system(const ArmState<T>& st, T (&A)[6][8]) {
@@ -636,14 +741,8 @@ IKG_HD inline void arm_system(const ArmState<T>& st, T (&A)[6][8]) {
     A[4][col] = st.ax[j][1];
     A[5][col] = st.ax[j][2];
   }
-  T ev[3], ew[3];
-  matvec3(st.Rh, st.e, ev);
-  matvec3(st.Rh, st.e + 3, ew);
 #pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    A[r][6] = ev[r];
-    A[3 + r][6] = ew[r];
-  }
+  for (int r = 0; r < 6; ++r) A[r][6] = st.e[r];
 }
 
 template <typename T>
@@ -683,9 +782,9 @@ IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b
 template <typename T>
 IKG_HD inline void arm_solve_wrist(const ArmState<T>& st, T* u, T* v) {
   const T* w = st.org[5];
-  T ev[3], ew[3], bl[3], wh[3], tmp[3];
-  matvec3(st.Rh, st.e, ev);
-  matvec3(st.Rh, st.e + 3, ew);
+  const T* ev = st.e;
+  const T* ew = st.e + 3;
+  T bl[3], wh[3], tmp[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) wh[i] = w[i] - st.th[i];
   cross3(ew, wh, tmp);

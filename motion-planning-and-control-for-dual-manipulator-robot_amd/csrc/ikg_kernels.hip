@@ -199,7 +199,7 @@ __global__ __launch_bounds__(256) void ikg_fk_kernel(const KModel<T>* __restrict
     T qc, qa[kArmDof], Rh[9], th[3], sn[7], cs[7];
     load_q(m, arm, qrow, qc, qa);
     trig_exact(qc, qa, sn, cs);
-    fk_arm<T, SpecGeneric, false>(m, arm, sn, cs, Rh, th, nullptr, nullptr);
+    fk_arm_world<T, SpecGeneric>(m, arm, sn, cs, Rh, th);
     T* out = hands + p * 24 + arm * 12;
 #pragma unroll
     for (int i = 0; i < 9; ++i) out[i] = Rh[i];
@@ -225,13 +225,16 @@ __global__ __launch_bounds__(64) void ikg_pair_state_kernel(const KModel<T>* __r
   load_q(m, arm, q0 + p * q0_stride, qc, qa);
   trig_exact(qc, qa, sn, cs);
   ArmState<T> st;
-  const T nrm = arm_fk_error<T, SpecGeneric>(m, arm, sn, cs, RT, tT, st);
+  const T nrm = arm_fk_error<T, SpecGeneric, false, true>(m, arm, sn, cs, RT, tT, st);
+  T el[6];  // world-aligned -> the reference's LOCAL error
+  matvec3_t(st.Rh, st.e, el);
+  matvec3_t(st.Rh, st.e + 3, el + 3);
   T* o = out + gid * 31;
   for (int i = 0; i < 9; ++i) o[i] = RT[i];
   for (int i = 0; i < 3; ++i) o[9 + i] = tT[i];
   for (int i = 0; i < 9; ++i) o[12 + i] = st.Rh[i];
   for (int i = 0; i < 3; ++i) o[21 + i] = st.th[i];
-  for (int i = 0; i < 6; ++i) o[24 + i] = st.e[i];
+  for (int i = 0; i < 6; ++i) o[24 + i] = el[i];
   o[30] = nrm;
 }
 

@@ -94,6 +94,17 @@ inline void build_kmodel(const ikg_model_desc& d, KModel<T>& k) {
       if (i != d.axis[q5] && d.placement[q5][9 + i] != 0.0) k.wrist = 0;
     }
   }
+  // zero placement offsets shared by both arms (Spec zero mask)
+  k.zmask = 0;
+  for (int j = 0; j < IKG_ARM_DOF; ++j)
+    for (int i = 0; i < 3; ++i)
+      if (d.placement[d.arm_q[0][j]][9 + i] == 0.0 && d.placement[d.arm_q[1][j]][9 + i] == 0.0)
+        k.zmask |= 1 << (3 * j + i);
+  for (int a = 0; a < 2; ++a)
+    for (int i = 0; i < 3; ++i) {
+      const double* H = d.hand[a];
+      k.hand_tH[a][i] = (T)(H[i] * H[9] + H[3 + i] * H[10] + H[6 + i] * H[11]);
+    }
   int pat = d.axis[r];
   for (int j = 0; j < IKG_ARM_DOF; ++j) pat |= d.axis[d.arm_q[0][j]] << (2 * (j + 1));
   pat |= k.hand_axis << 14;
@@ -103,7 +114,8 @@ inline void build_kmodel(const ikg_model_desc& d, KModel<T>& k) {
 // The compiled specialisation this model can use (ikg_launch.hpp kSpec*).
 template <typename T>
 inline int choose_spec(const KModel<T>& k) {
-  if (k.pattern == kPatternNextage && k.rot_mask == 0 && k.wrist) return 1;  // kSpecNextage
+  if (k.pattern == kPatternNextage && k.rot_mask == 0 && k.wrist && (k.zmask & kZeroNextage) == kZeroNextage)
+    return 1;  // kSpecNextage
   return 0;                                                                   // kSpecGeneric
 }
 
