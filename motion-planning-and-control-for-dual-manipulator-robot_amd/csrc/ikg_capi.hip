@@ -186,12 +186,7 @@ int check_params(const ikg_params* p) {
 
 template <typename T>
 ikg::KParams<T> kparams(const ikg_params* p) {
-  ikg::KParams<T> k;
-  k.eps = (T)p->eps;
-  k.dt = (T)p->dt;
-  k.lambda = (T)p->lambda;
-  k.max_iters = p->max_iters;
-  return k;
+  return ikg::make_kparams<T>(p);
 }
 
 template <typename T>

@@ -394,9 +394,9 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
     T dq[6], s = T(0);
     if (active && li < 2) {
       ArmState<T> st;
-      nrm = arm_fk_error<T, SP, true>(m, arm, sn, cs, RT, tT, st, V.F);
+      nrm = arm_fk_error<T, SP, true>(m, arm, sn, cs, RT, tT, st, V.F);  // squared
       const T other = pair_swap(nrm);
-      if (li == 0) V.flag[0] = (nrm < prm.eps && other < prm.eps) ? T(1) : T(0);
+      if (li == 0) V.flag[0] = (nrm < prm.eps2 && other < prm.eps2) ? T(1) : T(0);
       T alpha, beta;
       if constexpr (!DAMPED) {
         T u[6], v[6];
@@ -463,7 +463,7 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
 #endif
   if (started) {
     for (int j = li; j < nq; j += LG) q_out[p * nq + j] = V.q[j];
-    if (li < 2) err[p * 2 + arm] = nrm;
+    if (li < 2) err[p * 2 + arm] = sqrt(nrm);
     if (li == 0) {
       conv[p] = success ? 1 : 0;
       iters[p] = it;

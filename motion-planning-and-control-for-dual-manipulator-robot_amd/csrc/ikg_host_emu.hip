@@ -56,11 +56,11 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
     for (int arm = 0; arm < 2; ++arm)
       nrm[arm] = arm_fk_error<T, SP>(&m, arm, sn[arm], cs[arm], RT[arm], tT[arm], st[arm]);
     if (trace && it < trace_len) {
-      trace[2 * it] = nrm[0];
-      trace[2 * it + 1] = nrm[1];
+      trace[2 * it] = std::sqrt(nrm[0]);
+      trace[2 * it + 1] = std::sqrt(nrm[1]);
     }
     if (it >= prm.max_iters) break;
-    if (nrm[0] < prm.eps && nrm[1] < prm.eps) {
+    if (nrm[0] < prm.eps2 && nrm[1] < prm.eps2) {
       if (!col) {
         conv = true;
         break;
@@ -111,8 +111,8 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
     for (int k = 0; k < kArmDof; ++k) qo[m.arm_q[arm][k]] = qa[arm][k];
   *conv_out = conv;
   *iters_out = it;
-  err_out[0] = nrm[0];
-  err_out[1] = nrm[1];
+  err_out[0] = std::sqrt(nrm[0]);
+  err_out[1] = std::sqrt(nrm[1]);
 }
 
 template <typename T>
@@ -127,7 +127,7 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
     ikg::build_kcollision<T>(*cd, kc);
     col = &kc;
   }
-  ikg::KParams<T> prm{(T)p->eps, (T)p->dt, (T)p->lambda, p->max_iters};
+  const ikg::KParams<T> prm = ikg::make_kparams<T>(p);
   const bool special = p->variant != 99 && ikg::choose_spec(m) == 1;  // variant 99: force generic
   for (int64_t i = 0; i < B; ++i) {
     const T* tg = (const T*)targets + 12 * i;

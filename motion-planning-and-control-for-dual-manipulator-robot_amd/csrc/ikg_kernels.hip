@@ -37,20 +37,16 @@ __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams
   trig_exact(qc, qa, sn, cs);
   int it = 0;
   bool conv = false;
-  T nrm, other;
+  T x, xo;  // squared error norms of this lane's hand and the partner's
+  ThetaTrack<T> tk{};
   for (;;) {
     ArmState<T> st;
-    nrm = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
-    other = pair_swap(nrm);
-    if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
-    if (nrm < prm.eps && other < prm.eps) {
-      conv = true;
-      break;
-    }
-    T q_old[7];
-    q_old[0] = qc;
-#pragma unroll
-    for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
+    if constexpr (IKG_THETA_TRACK && sizeof(T) == 8)  // fp32: atan2f is as cheap (measured)
+      x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, &tk, (it % Trig<T>::kResync) == 0);
+    else
+      x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
+    // the step is formed before the stop test (discarded when the loop ends)
+    // so the test's exchange/compare overlaps the solve instead of heading it
     T dq[6], alpha, beta, s;
     if constexpr (!DAMPED) {
       T u[6], v[6];
@@ -64,13 +60,23 @@ __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams
       s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
       arm_dq_damped(A, ze, zc, s, dq);
     }
+    xo = pair_swap(x);
+    if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
+    if (x < prm.eps2 && xo < prm.eps2) {  // |e_L| < eps and |e_R| < eps (:70)
+      conv = true;
+      break;
+    }
+    T q_old[7];
+    q_old[0] = qc;
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
     arm_update(m, arm, prm.dt, s, dq, qc, qa);
     ++it;
     trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }
   it_out = it;
-  nrm_out = nrm;
-  other_out = other;
+  nrm_out = sqrt(x);
+  other_out = sqrt(xo);
   conv_out = conv;
 }
 
@@ -225,7 +231,7 @@ __global__ __launch_bounds__(64) void ikg_pair_state_kernel(const KModel<T>* __r
   load_q(m, arm, q0 + p * q0_stride, qc, qa);
   trig_exact(qc, qa, sn, cs);
   ArmState<T> st;
-  const T nrm = arm_fk_error<T, SpecGeneric, false, true>(m, arm, sn, cs, RT, tT, st);
+  const T nrm = sqrt(arm_fk_error<T, SpecGeneric, false, true>(m, arm, sn, cs, RT, tT, st));
   T el[6];  // world-aligned -> the reference's LOCAL error
   matvec3_t(st.Rh, st.e, el);
   matvec3_t(st.Rh, st.e + 3, el + 3);

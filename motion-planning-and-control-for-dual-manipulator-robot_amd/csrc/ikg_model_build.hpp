@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <limits>
 
 #include "ikg_collision.hpp"
 #include "ikg_device.hpp"
@@ -109,6 +110,28 @@ inline void build_kmodel(const ikg_model_desc& d, KModel<T>& k) {
   for (int j = 0; j < IKG_ARM_DOF; ++j) pat |= d.axis[d.arm_q[0][j]] << (2 * (j + 1));
   pat |= k.hand_axis << 14;
   k.pattern = pat;
+}
+
+// Smallest x with sqrt(x) >= eps (both in T, IEEE): the loop tests x < eps2,
+// which is exactly sqrt(x) < eps for a correctly rounded sqrt.
+template <typename T>
+inline T stop_threshold(T eps) {
+  if (!(eps > T(0))) return T(0);
+  T m = eps * eps;
+  while (m > T(0) && std::sqrt(m) >= eps) m = std::nextafter(m, T(0));
+  while (std::sqrt(m) < eps) m = std::nextafter(m, std::numeric_limits<T>::max());
+  return m;
+}
+
+template <typename T>
+inline KParams<T> make_kparams(const ikg_params* p) {
+  KParams<T> k;
+  k.eps = (T)p->eps;
+  k.dt = (T)p->dt;
+  k.lambda = (T)p->lambda;
+  k.max_iters = p->max_iters;
+  k.eps2 = stop_threshold<T>((T)p->eps);
+  return k;
 }
 
 // The compiled specialisation this model can use (ikg_launch.hpp kSpec*).
