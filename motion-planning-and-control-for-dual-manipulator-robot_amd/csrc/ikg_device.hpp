@@ -1029,9 +1029,13 @@ IKG_HD inline void arm_update(const KModel<T>* __restrict__ m, int arm, T dt, T 
   qc = clampq(qc + s * dt, m->root_lo, m->root_hi);
 #pragma unroll
   for (int k = 0; k < kArmDof; ++k) {
-    const T lo = sel(right, m->arm_lo[1][k], m->arm_lo[0][k]);
-    const T hi = sel(right, m->arm_hi[1][k], m->arm_hi[0][k]);
-    qa[k] = clampq(qa[k] + dq[k] * dt, lo, hi);
+    // clamp against both arms' (scalar) limits and select the result: 2 VALU
+    // ops per bound with scalar operands instead of materialising per-lane
+    // limits (the pair kernel has no registers to keep them)
+    const T v = qa[k] + dq[k] * dt;
+    const T qL = clampq(v, m->arm_lo[0][k], m->arm_hi[0][k]);
+    const T qR = clampq(v, m->arm_lo[1][k], m->arm_hi[1][k]);
+    qa[k] = sel(right, qR, qL);
   }
 }
 
