@@ -163,6 +163,47 @@ IKG_HD inline T fdiv(T a, T b) {
 #endif
 }
 
+// 1 / b (same refinement as fdiv, ~1 ulp)
+template <typename T>
+IKG_HD inline T frcp(T b) {
+#ifdef __HIP_DEVICE_COMPILE__
+  if constexpr (sizeof(T) == 8) {
+    double r = __builtin_amdgcn_rcp(b);
+    r = fma(r, fma(-b, r, 1.0), r);
+    r = fma(r, fma(-b, r, 1.0), r);
+    return fma(r, fma(-b, r, 1.0), r);
+  } else {
+    float r = __builtin_amdgcn_rcpf(b);
+    return fmaf(r, fmaf(-b, r, 1.0f), r);
+  }
+#else
+  return T(1) / b;
+#endif
+}
+
+// sqrt(x) for 0 <= x <= 4 (|skew| of a rotation): OCML's refinement without
+// its denormal scaling and special-value selects (x = 0 gives 0)
+template <typename T>
+IKG_HD inline T fsqrt_unit(T x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  if constexpr (sizeof(T) == 8) {
+    const double y = __builtin_amdgcn_rsq(fmax(x, 1e-300));
+    double g = x * y, h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    return fma(d, h, g);
+  } else {
+    return sqrtf(x);
+  }
+#else
+  return std::sqrt(x);
+#endif
+}
+
 // ---------------------------------------------------------------- cross-lane
 // Exchange a value with the partner lane (lane ^ 1) through a DPP quad_perm
 // [1,0,3,2]: no LDS traffic, one VALU op per dword.
@@ -376,7 +417,7 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
   const T tr = R[0] + R[4] + R[8];
   const T sx = R[7] - R[5], sy = R[2] - R[6], sz = R[3] - R[1];
   const T ct = (tr - T(1)) * T(0.5);
-  const T st = sqrt(sx * sx + sy * sy + sz * sz) * T(0.5);
+  const T st = fsqrt_unit(sx * sx + sy * sy + sz * sz) * T(0.5);
   T theta = T(0);
   bool exact = true;
   if (tk && !resync) {
@@ -405,32 +446,37 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
   const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-30);
   const bool above = theta > Prec<T>::kPrec3;
   const bool below = theta < Prec<T>::kPrec3;
+  // one reciprocal serves theta/sin(theta) and 1/theta^2: q = 1/(theta^2 sin)
+  const T q = frcp<T>(fmax(t2 * st, tiny));
+  const T inv_t2 = st * q;
   T f;
   if constexpr (sizeof(T) == 8)
-    f = above ? fdiv<T>(theta, fmax(st, tiny)) : T(1);  // Pinocchio: theta/sin(theta) -> 1 below precision<3>()
+    f = above ? theta * t2 * q : T(1);  // Pinocchio: theta/sin(theta) -> 1 below precision<3>()
   else
-    f = above ? fdiv<T>(theta, fmax(st, tiny)) : T(1) + t2 * (T(1) / T(6) + t2 * (T(7) / T(360)));
+    f = above ? theta * t2 * q : T(1) + t2 * (T(1) / T(6) + t2 * (T(7) / T(360)));
   const T hf = f * T(0.5);
   T w[3] = {hf * sx, hf * sy, hf * sz};
-  // theta (1+cos)/(2 sin) for cos >= 0, theta sin/(2(1-cos)) otherwise: no cancellation
-  T alpha = ct >= T(0) ? hf * (T(1) + ct) : fdiv<T>(theta * st, T(2) * fmax(T(1) - ct, tiny));
-  if (theta >= pi - T(1e-2)) {  // near pi: the axis from the diagonal (rare)
+  // alpha = theta sin/(2(1-cos)) = theta (1+cos)/(2 sin): the second form has no
+  // cancellation below the near-pi band (there |1+cos| >= 5e-5: < 2e-14 abs.)
+  T alpha = hf * (T(1) + ct);
+  if (theta >= pi - T(1e-2)) {  // near pi (rare): the axis from the diagonal
     const T beta = fdiv<T>(t2, T(1) - ct);
     const T t0 = (R[0] - ct) * beta, t1 = (R[4] - ct) * beta, tt = (R[8] - ct) * beta;
     w[0] = (R[7] > R[5] ? T(1) : T(-1)) * (t0 > T(0) ? sqrt(t0) : T(0));
     w[1] = (R[2] > R[6] ? T(1) : T(-1)) * (t1 > T(0) ? sqrt(t1) : T(0));
     w[2] = (R[3] > R[1] ? T(1) : T(-1)) * (tt > T(0) ? sqrt(tt) : T(0));
+    alpha = fdiv<T>(theta * st, T(2) * (T(1) - ct));
   }
   T beta;
   if constexpr (sizeof(T) == 8) {
     const T as = T(1) - t2 / T(12) - t2 * t2 / T(720);
     const T bs = T(1) / T(12) + t2 / T(720);
-    beta = below ? bs : fdiv<T>(T(1) - alpha, fmax(t2, tiny));
+    beta = below ? bs : (T(1) - alpha) * inv_t2;
     alpha = below ? as : alpha;
   } else {
     const T as = T(1) - t2 * (T(1) / T(12) + t2 * (T(1) / T(720) + t2 * (T(1) / T(30240))));
     const T bs = T(1) / T(12) + t2 * (T(1) / T(720) + t2 * (T(1) / T(30240) + t2 * (T(1) / T(1209600))));
-    beta = below ? bs : fdiv<T>(T(1) - alpha, fmax(t2, tiny));
+    beta = below ? bs : (T(1) - alpha) * inv_t2;
     alpha = below ? as : alpha;
   }
   const T wp = w[0] * p[0] + w[1] * p[1] + w[2] * p[2];
@@ -897,7 +943,7 @@ IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b
   cross3(g3, g1, r2);
   cross3(g1, g2, r3);
   const T det = dot3(g1, r1);
-  const T rdet = det != T(0) ? fdiv(T(1), det) : T(0);
+  const T rdet = det != T(0) ? frcp(det) : T(0);
   x0[0] = dot3(r1, b0) * rdet;
   x0[1] = dot3(r2, b0) * rdet;
   x0[2] = dot3(r3, b0) * rdet;
