@@ -28,6 +28,10 @@
 #ifndef IKG_THETA_TRACK
 #define IKG_THETA_TRACK 1
 #endif
+// angle increment by a division-free asin series (1) or atan(y/x) (0)
+#ifndef IKG_THETA_ASIN
+#define IKG_THETA_ASIN 1
+#endif
 
 namespace ikg {
 
@@ -401,6 +405,13 @@ struct ThetaInc<double> {
     const double r2 = r * r;
     return r + r * r2 * (-1.0 / 3 + r2 * (1.0 / 5 + r2 * (-1.0 / 7 + r2 * (1.0 / 9 + r2 * (-1.0 / 11)))));
   }
+  // |y| <= 0.035 (the angle moves ~1% of itself per update): the first dropped
+  // term 63/2816 y^11 < 3e-18
+  static constexpr double kIncAsin = 0.035;
+  IKG_HD static inline double asin_small(double y) {
+    const double y2 = y * y;
+    return y + y * y2 * (1.0 / 6 + y2 * (3.0 / 40 + y2 * (5.0 / 112 + y2 * (35.0 / 1152))));
+  }
 };
 template <>
 struct ThetaInc<float> {
@@ -408,6 +419,11 @@ struct ThetaInc<float> {
   IKG_HD static inline float atan_small(float r) {
     const float r2 = r * r;
     return r + r * r2 * (-1.0f / 3 + r2 * (1.0f / 5 + r2 * (-1.0f / 7)));
+  }
+  static constexpr float kIncAsin = 0.035f;
+  IKG_HD static inline float asin_small(float y) {
+    const float y2 = y * y;
+    return y + y * y2 * (1.0f / 6 + y2 * (3.0f / 40));
   }
 };
 
@@ -423,8 +439,15 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
   if (tk && !resync) {
     const T y = st * tk->ct - ct * tk->st;  // rho sin(theta - theta_prev)
     const T x = ct * tk->ct + st * tk->st;  // rho cos(theta - theta_prev)
+#if IKG_THETA_ASIN
+    // rho = |(st, ct)| |(st', ct')| = 1 up to the rotations' rounding (~1e-15),
+    // so delta = asin(y) to that relative accuracy: a division-free series
+    exact = !(fabs(y) <= ThetaInc<T>::kIncAsin && x > T(0));
+    theta = tk->th + ThetaInc<T>::asin_small(y);
+#else
     exact = !(fabs(y) <= ThetaInc<T>::kInc * x);
     theta = tk->th + ThetaInc<T>::atan_small(fdiv<T>(y, fmax(x, T(1e-30))));
+#endif
   }
   if (exact) {
     if constexpr (sizeof(T) == 8) {
@@ -499,7 +522,7 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
 template <typename T>
 struct Trig;
 #ifndef IKG_RESYNC64
-#define IKG_RESYNC64 32
+#define IKG_RESYNC64 128
 #endif
 template <>
 struct Trig<double> {
