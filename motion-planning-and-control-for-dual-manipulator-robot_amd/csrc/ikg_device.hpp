@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 // Math helpers are __host__ __device__ so tools/host_emu.cpp can run the
 // exact kernel arithmetic on the CPU for debugging (never a product path).
 #define IKG_HD __host__ __device__
@@ -115,6 +117,69 @@ struct KParams {
   T eps2;
 };
 
+// ---------------------------------------------------------------- lane value types
+// Scalar kernels (pair layout: one arm per lane) use T = double / float.  The
+// packed fp32 kernel keeps BOTH arms of a problem in one lane as a 2-vector
+// (x = left, y = right) so each v_pk_{fma,mul,add}_f32 advances both arms; the
+// shared root joint is carried in both halves.  The helpers below give the
+// iteration code one spelling for both (masks, selects, per-arm constants).
+typedef float v2f __attribute__((ext_vector_type(2)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+template <typename T>
+struct LaneT {
+  using E = T;     // element type
+  using M = bool;  // comparison mask
+  static constexpr bool packed = false;
+};
+template <>
+struct LaneT<v2f> {
+  using E = float;
+  using M = v2i;
+  static constexpr bool packed = true;
+};
+template <typename T>
+constexpr bool is_f64 = std::is_same<typename LaneT<T>::E, double>::value;
+template <typename T>
+constexpr bool is_packed = LaneT<T>::packed;
+
+IKG_HD inline bool any_of(bool m) { return m; }
+IKG_HD inline bool any_of(v2i m) { return m.x != 0 || m.y != 0; }
+IKG_HD inline bool all_of(bool m) { return m; }
+IKG_HD inline bool all_of(v2i m) { return m.x != 0 && m.y != 0; }
+IKG_HD inline bool mnot(bool m) { return !m; }
+IKG_HD inline v2i mnot(v2i m) { return m == 0; }
+template <typename T, typename M>
+IKG_HD inline T vsel(M m, T a, T b) {
+  if constexpr (LaneT<T>::packed)
+    return T{m.x ? a.x : b.x, m.y ? a.y : b.y};
+  else
+    return m ? a : b;
+}
+
+// per-arm model constant: the lane's arm (pair layout) or both (packed)
+template <typename T, typename E>
+IKG_HD inline T armc(bool right, E left_v, E right_v) {
+  if constexpr (is_packed<T>)
+    return T{left_v, right_v};
+  else
+    return right ? right_v : left_v;
+}
+
+// elementwise math on the packed type (the global overloads stay visible)
+using ::atan2;
+using ::atan2f;
+using ::fabs;
+using ::fmax;
+using ::fmin;
+using ::sqrt;
+IKG_HD inline v2f fmax(v2f a, v2f b) { return v2f{::fmaxf(a.x, b.x), ::fmaxf(a.y, b.y)}; }
+IKG_HD inline v2f fmin(v2f a, v2f b) { return v2f{::fminf(a.x, b.x), ::fminf(a.y, b.y)}; }
+IKG_HD inline v2f fabs(v2f a) { return v2f{::fabsf(a.x), ::fabsf(a.y)}; }
+IKG_HD inline v2f sqrt(v2f a) { return v2f{::sqrtf(a.x), ::sqrtf(a.y)}; }
+IKG_HD inline v2f atan2(v2f y, v2f x) { return v2f{::atan2f(y.x, x.x), ::atan2f(y.y, x.y)}; }
+IKG_HD inline v2f atan2f(v2f y, v2f x) { return atan2(y, x); }
+
 // ---------------------------------------------------------------- precision traits
 template <typename T>
 struct Prec;
@@ -140,6 +205,20 @@ struct Prec<float> {
   IKG_HD static inline void sincos_(float x, float* s, float* c) { ::sincosf(x, s, c); }
 };
 
+template <>
+struct Prec<v2f> {
+  static constexpr float kPrec3 = Prec<float>::kPrec3;
+  static constexpr float kPi = Prec<float>::kPi;
+  static constexpr float kRcond = Prec<float>::kRcond;
+  IKG_HD static inline void sincos_(v2f x, v2f* s, v2f* c) {
+    float s0, c0, s1, c1;
+    ::sincosf(x.x, &s0, &c0);
+    ::sincosf(x.y, &s1, &c1);
+    *s = v2f{s0, s1};
+    *c = v2f{c0, c1};
+  }
+};
+
 template <typename T>
 IKG_HD inline T sel(bool b, T x, T y) { return b ? x : y; }
 
@@ -150,12 +229,17 @@ IKG_HD inline T sel(bool b, T x, T y) { return b ? x : y; }
 template <typename T>
 IKG_HD inline T fdiv(T a, T b) {
 #ifdef __HIP_DEVICE_COMPILE__
-  if constexpr (sizeof(T) == 8) {
+  if constexpr (is_f64<T>) {
     double r = __builtin_amdgcn_rcp(b);
     r = fma(r, fma(-b, r, 1.0), r);
     r = fma(r, fma(-b, r, 1.0), r);
     const double q = a * r;
     return fma(fma(-b, q, a), r, q);
+  } else if constexpr (is_packed<T>) {
+    v2f r = v2f{__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+    r = r * (-b * r + 1.0f) + r;
+    const v2f q = a * r;
+    return (-b * q + a) * r + q;
   } else {
     float r = __builtin_amdgcn_rcpf(b);
     r = fmaf(r, fmaf(-b, r, 1.0f), r);
@@ -171,11 +255,14 @@ IKG_HD inline T fdiv(T a, T b) {
 template <typename T>
 IKG_HD inline T frcp(T b) {
 #ifdef __HIP_DEVICE_COMPILE__
-  if constexpr (sizeof(T) == 8) {
+  if constexpr (is_f64<T>) {
     double r = __builtin_amdgcn_rcp(b);
     r = fma(r, fma(-b, r, 1.0), r);
     r = fma(r, fma(-b, r, 1.0), r);
     return fma(r, fma(-b, r, 1.0), r);
+  } else if constexpr (is_packed<T>) {
+    const v2f r = v2f{__builtin_amdgcn_rcpf(b.x), __builtin_amdgcn_rcpf(b.y)};
+    return r * (-b * r + 1.0f) + r;
   } else {
     float r = __builtin_amdgcn_rcpf(b);
     return fmaf(r, fmaf(-b, r, 1.0f), r);
@@ -190,7 +277,7 @@ IKG_HD inline T frcp(T b) {
 template <typename T>
 IKG_HD inline T fsqrt_unit(T x) {
 #ifdef __HIP_DEVICE_COMPILE__
-  if constexpr (sizeof(T) == 8) {
+  if constexpr (is_f64<T>) {
     const double y = __builtin_amdgcn_rsq(fmax(x, 1e-300));
     double g = x * y, h = y * 0.5;
     const double r = fma(-h, g, 0.5);
@@ -201,10 +288,13 @@ IKG_HD inline T fsqrt_unit(T x) {
     d = fma(-g, g, x);
     return fma(d, h, g);
   } else {
-    return sqrtf(x);
+    return sqrt(x);
   }
 #else
-  return std::sqrt(x);
+  if constexpr (is_packed<T>)
+    return sqrt(x);
+  else
+    return std::sqrt(x);
 #endif
 }
 
@@ -223,6 +313,8 @@ __device__ inline double pair_swap(double x) {
   hi = pair_swap_i32(hi);
   return __hiloint2double(hi, lo);
 }
+// packed: the partner arm is the other half of the same lane
+IKG_HD inline v2f pair_swap(v2f x) { return x.yx; }
 
 // ---------------------------------------------------------------- SE(3) pieces
 // R is row-major: R[3*r + c].
@@ -429,78 +521,83 @@ struct ThetaInc<float> {
 
 template <typename T>
 IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = nullptr, bool resync = true) {
-  const T pi = Prec<T>::kPi;
+  using M = typename LaneT<T>::M;
+  const T pi = T(Prec<T>::kPi);
   const T tr = R[0] + R[4] + R[8];
   const T sx = R[7] - R[5], sy = R[2] - R[6], sz = R[3] - R[1];
   const T ct = (tr - T(1)) * T(0.5);
   const T st = fsqrt_unit(sx * sx + sy * sy + sz * sz) * T(0.5);
   T theta = T(0);
-  bool exact = true;
-  if (tk && !resync) {
-    const T y = st * tk->ct - ct * tk->st;  // rho sin(theta - theta_prev)
-    const T x = ct * tk->ct + st * tk->st;  // rho cos(theta - theta_prev)
+  if constexpr (is_f64<T>) {
+    bool exact = true;
+    if (tk && !resync) {
+      const T y = st * tk->ct - ct * tk->st;  // rho sin(theta - theta_prev)
+      const T x = ct * tk->ct + st * tk->st;  // rho cos(theta - theta_prev)
 #if IKG_THETA_ASIN
-    // rho = |(st, ct)| |(st', ct')| = 1 up to the rotations' rounding (~1e-15),
-    // so delta = asin(y) to that relative accuracy: a division-free series
-    exact = !(fabs(y) <= ThetaInc<T>::kIncAsin && x > T(0));
-    theta = tk->th + ThetaInc<T>::asin_small(y);
+      // rho = |(st, ct)| |(st', ct')| = 1 up to the rotations' rounding (~1e-15),
+      // so delta = asin(y) to that relative accuracy: a division-free series
+      exact = !(fabs(y) <= ThetaInc<T>::kIncAsin && x > T(0));
+      theta = tk->th + ThetaInc<T>::asin_small(y);
 #else
-    exact = !(fabs(y) <= ThetaInc<T>::kInc * x);
-    theta = tk->th + ThetaInc<T>::atan_small(fdiv<T>(y, fmax(x, T(1e-30))));
+      exact = !(fabs(y) <= ThetaInc<T>::kInc * x);
+      theta = tk->th + ThetaInc<T>::atan_small(fdiv<T>(y, fmax(x, T(1e-30))));
 #endif
-  }
-  if (exact) {
-    if constexpr (sizeof(T) == 8) {
+    }
+    if (exact) {
 #if IKG_THETA == 1
       theta = atan2(st, ct);
 #else
       theta = acos(fmin(fmax(ct, T(-1)), T(1)));  // pin.log3: tr > 3 -> 0, tr < -1 -> pi
 #endif
-    } else {
-      theta = atan2f(st, ct);  // fp32: accurate near 0 where acos is not
     }
-  }
-  if (tk) {
-    tk->th = theta;
-    tk->st = st;
-    tk->ct = ct;
+    if (tk) {
+      tk->th = theta;
+      tk->st = st;
+      tk->ct = ct;
+    }
+  } else {
+    theta = atan2f(st, ct);  // fp32: accurate near 0 where acos is not
   }
   const T t2 = theta * theta;
-  const T tiny = sizeof(T) == 8 ? T(1e-300) : T(1e-30);
-  const bool above = theta > Prec<T>::kPrec3;
-  const bool below = theta < Prec<T>::kPrec3;
+  const T tiny = is_f64<T> ? T(1e-300) : T(1e-30f);
+  const M above = theta > T(Prec<T>::kPrec3);
+  const M below = theta < T(Prec<T>::kPrec3);
   // one reciprocal serves theta/sin(theta) and 1/theta^2: q = 1/(theta^2 sin)
   const T q = frcp<T>(fmax(t2 * st, tiny));
   const T inv_t2 = st * q;
   T f;
-  if constexpr (sizeof(T) == 8)
-    f = above ? theta * t2 * q : T(1);  // Pinocchio: theta/sin(theta) -> 1 below precision<3>()
+  if constexpr (is_f64<T>)
+    f = vsel<T>(above, theta * t2 * q, T(1));  // Pinocchio: theta/sin(theta) -> 1 below precision<3>()
   else
-    f = above ? theta * t2 * q : T(1) + t2 * (T(1) / T(6) + t2 * (T(7) / T(360)));
+    f = vsel<T>(above, theta * t2 * q, T(1) + t2 * (T(1.f / 6) + t2 * T(7.f / 360)));
   const T hf = f * T(0.5);
   T w[3] = {hf * sx, hf * sy, hf * sz};
   // alpha = theta sin/(2(1-cos)) = theta (1+cos)/(2 sin): the second form has no
   // cancellation below the near-pi band (there |1+cos| >= 5e-5: < 2e-14 abs.)
   T alpha = hf * (T(1) + ct);
-  if (theta >= pi - T(1e-2)) {  // near pi (rare): the axis from the diagonal
+  const M near_pi = theta >= pi - T(1e-2);
+  if (any_of(near_pi)) {  // near pi (rare): the axis from the diagonal
     const T beta = fdiv<T>(t2, T(1) - ct);
     const T t0 = (R[0] - ct) * beta, t1 = (R[4] - ct) * beta, tt = (R[8] - ct) * beta;
-    w[0] = (R[7] > R[5] ? T(1) : T(-1)) * (t0 > T(0) ? sqrt(t0) : T(0));
-    w[1] = (R[2] > R[6] ? T(1) : T(-1)) * (t1 > T(0) ? sqrt(t1) : T(0));
-    w[2] = (R[3] > R[1] ? T(1) : T(-1)) * (tt > T(0) ? sqrt(tt) : T(0));
-    alpha = fdiv<T>(theta * st, T(2) * (T(1) - ct));
+    const T wp0 = vsel<T>(R[7] > R[5], T(1), T(-1)) * vsel<T>(t0 > T(0), sqrt(t0), T(0));
+    const T wp1 = vsel<T>(R[2] > R[6], T(1), T(-1)) * vsel<T>(t1 > T(0), sqrt(t1), T(0));
+    const T wp2 = vsel<T>(R[3] > R[1], T(1), T(-1)) * vsel<T>(tt > T(0), sqrt(tt), T(0));
+    w[0] = vsel<T>(near_pi, wp0, w[0]);
+    w[1] = vsel<T>(near_pi, wp1, w[1]);
+    w[2] = vsel<T>(near_pi, wp2, w[2]);
+    alpha = vsel<T>(near_pi, fdiv<T>(theta * st, T(2) * (T(1) - ct)), alpha);
   }
   T beta;
-  if constexpr (sizeof(T) == 8) {
+  if constexpr (is_f64<T>) {
     const T as = T(1) - t2 / T(12) - t2 * t2 / T(720);
     const T bs = T(1) / T(12) + t2 / T(720);
-    beta = below ? bs : (T(1) - alpha) * inv_t2;
-    alpha = below ? as : alpha;
+    beta = vsel<T>(below, bs, (T(1) - alpha) * inv_t2);
+    alpha = vsel<T>(below, as, alpha);
   } else {
-    const T as = T(1) - t2 * (T(1) / T(12) + t2 * (T(1) / T(720) + t2 * (T(1) / T(30240))));
-    const T bs = T(1) / T(12) + t2 * (T(1) / T(720) + t2 * (T(1) / T(30240) + t2 * (T(1) / T(1209600))));
-    beta = below ? bs : (T(1) - alpha) * inv_t2;
-    alpha = below ? as : alpha;
+    const T as = T(1) - t2 * (T(1.f / 12) + t2 * (T(1.f / 720) + t2 * T(1.f / 30240)));
+    const T bs = T(1.f / 12) + t2 * (T(1.f / 720) + t2 * (T(1.f / 30240) + t2 * T(1.f / 1209600)));
+    beta = vsel<T>(below, bs, (T(1) - alpha) * inv_t2);
+    alpha = vsel<T>(below, as, alpha);
   }
   const T wp = w[0] * p[0] + w[1] * p[1] + w[2] * p[2];
   const T bwp = beta * wp;
@@ -552,6 +649,19 @@ struct Trig<float> {
     s = sn;
   }
 };
+template <>
+struct Trig<v2f> {
+  static constexpr float kIncMax = Trig<float>::kIncMax;
+  static constexpr int kResync = Trig<float>::kResync;
+  IKG_HD static inline void step(v2f d, v2f& s, v2f& c) {
+    const v2f d2 = d * d;
+    const v2f sd = d + d * d2 * (-1.0f / 6 + d2 * (1.0f / 120 + d2 * (-1.0f / 5040)));
+    const v2f cd = 1.0f + d2 * (-0.5f + d2 * (1.0f / 24 + d2 * (-1.0f / 720)));
+    const v2f sn = s * cd + c * sd;
+    c = c * cd - s * sd;
+    s = sn;
+  }
+};
 
 // ---------------------------------------------------------------- one arm's kinematics
 template <int AX, typename T>
@@ -574,7 +684,7 @@ IKG_HD inline void column_ax(const T* R, int runtime_axis, T* a) {
 // tc = root_t (the "chest frame"; setup_pinocchio.py:32 folds ROBOT_PLACEMENT
 // into root_t).
 template <typename T, class SP>
-IKG_HD inline void root_frame(const KModel<T>* __restrict__ m, T s0, T c0, T* Rc, T* tc) {
+IKG_HD inline void root_frame(const KModel<typename LaneT<T>::E>* __restrict__ m, T s0, T c0, T* Rc, T* tc) {
   if constexpr (SP::prot) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) Rc[i] = m->root_R[i];
@@ -599,7 +709,7 @@ IKG_HD inline void root_frame(const KModel<T>* __restrict__ m, T s0, T c0, T* Rc
 // chest frame: the root rotation and the arm's zero placement components fold
 // away at compile time (Spec).
 template <typename T, class SP, bool WANT_AXES, bool WANT_FRAMES = false>
-IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0, const T* t0, const T* sn,
+IKG_HD inline void fk_arm(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const T* R0, const T* t0, const T* sn,
                           const T* cs, T* Rh, T* th, T (*ax)[3], T (*org)[3], T (*frames)[12] = nullptr) {
   T R[9], t[3];
 #pragma unroll
@@ -628,7 +738,7 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0,
   for (int k = 0; k < kArmDof; ++k) {
     T pt[3], dt_[3];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) pt[i] = SP::zero_t(k, i) ? T(0) : sel(right, m->arm_t[1][k][i], m->arm_t[0][k][i]);
+    for (int i = 0; i < 3; ++i) pt[i] = SP::zero_t(k, i) ? T(0) : armc<T>(right, m->arm_t[0][k][i], m->arm_t[1][k][i]);
     matvec3(R, pt, dt_);
 #pragma unroll
     for (int i = 0; i < 3; ++i) t[i] += dt_[i];
@@ -636,7 +746,7 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0,
       if (m->rot_mask & (1 << k)) {
         T P[9], Rn[9];
 #pragma unroll
-        for (int i = 0; i < 9; ++i) P[i] = sel(right, m->arm_R[1][k][i], m->arm_R[0][k][i]);
+        for (int i = 0; i < 9; ++i) P[i] = armc<T>(right, m->arm_R[0][k][i], m->arm_R[1][k][i]);
         matmul3(R, P, Rn);
 #pragma unroll
         for (int i = 0; i < 9; ++i) R[i] = Rn[i];
@@ -651,8 +761,8 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0,
       default:
         if constexpr (FOLD) {
           // Rot(q5) Rot(h) = Rot(q5 + h): (sin, cos) by angle addition
-          const T hs = sel(right, m->hand_sc[1][0], m->hand_sc[0][0]);
-          const T hc = sel(right, m->hand_sc[1][1], m->hand_sc[0][1]);
+          const T hs = armc<T>(right, m->hand_sc[0][0], m->hand_sc[1][0]);
+          const T hc = armc<T>(right, m->hand_sc[0][1], m->hand_sc[1][1]);
           rotate_axis(R, SP::axis(6), sn[6] * hc + cs[6] * hs, cs[6] * hc - sn[6] * hs);
         } else {
           rotate_ax<SP::axis(6)>(R, m->arm_axis[5], sn[6], cs[6]);
@@ -683,7 +793,7 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0,
   if constexpr (FOLD) {
     // R is already the hand rotation: th = t + R6 ht = t + Rh (hand_R^T ht)
 #pragma unroll
-    for (int i = 0; i < 3; ++i) ht[i] = sel(right, m->hand_tH[1][i], m->hand_tH[0][i]);
+    for (int i = 0; i < 3; ++i) ht[i] = armc<T>(right, m->hand_tH[0][i], m->hand_tH[1][i]);
     matvec3(R, ht, d);
 #pragma unroll
     for (int i = 0; i < 3; ++i) th[i] = t[i] + d[i];
@@ -691,7 +801,7 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0,
     for (int i = 0; i < 9; ++i) Rh[i] = R[i];
   } else {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) ht[i] = sel(right, m->hand_t[1][i], m->hand_t[0][i]);
+    for (int i = 0; i < 3; ++i) ht[i] = armc<T>(right, m->hand_t[0][i], m->hand_t[1][i]);
     matvec3(R, ht, d);
 #pragma unroll
     for (int i = 0; i < 3; ++i) th[i] = t[i] + d[i];
@@ -700,12 +810,12 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0,
       // hand placement rotation = R_axis(angle): two columns change
 #pragma unroll
       for (int i = 0; i < 9; ++i) Rh[i] = R[i];
-      rotate_axis(Rh, HA, sel(right, m->hand_sc[1][0], m->hand_sc[0][0]),
-                  sel(right, m->hand_sc[1][1], m->hand_sc[0][1]));
+      rotate_axis(Rh, HA, armc<T>(right, m->hand_sc[0][0], m->hand_sc[1][0]),
+                  armc<T>(right, m->hand_sc[0][1], m->hand_sc[1][1]));
     } else {
       T hR[9];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) hR[i] = sel(right, m->hand_R[1][i], m->hand_R[0][i]);
+      for (int i = 0; i < 9; ++i) hR[i] = armc<T>(right, m->hand_R[0][i], m->hand_R[1][i]);
       matmul3(R, hR, Rh);
     }
   }
@@ -713,7 +823,7 @@ IKG_HD inline void fk_arm(const KModel<T>* __restrict__ m, int arm, const T* R0,
 
 // World-frame FK of one arm (batch FK kernel, diagnostics).
 template <typename T, class SP>
-IKG_HD inline void fk_arm_world(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, T* Rh, T* th) {
+IKG_HD inline void fk_arm_world(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const T* sn, const T* cs, T* Rh, T* th) {
   T Rc[9], tc[3];
   root_frame<T, SP>(m, sn[0], cs[0], Rc, tc);
   fk_arm<T, SP, false>(m, arm, Rc, tc, sn, cs, Rh, th, nullptr, nullptr);
@@ -881,7 +991,7 @@ IKG_HD inline void trig_advance(T qc, const T* qa, const T* q_old, bool resync, 
 #pragma unroll
   for (int k = 0; k < kArmDof; ++k) d[k + 1] = qa[k] - q_old[k + 1];
 #pragma unroll
-  for (int j = 0; j < 7; ++j) big |= fabs(d[j]) > Trig<T>::kIncMax;
+  for (int j = 0; j < 7; ++j) big |= any_of(fabs(d[j]) > T(Trig<T>::kIncMax));
   if constexpr (IKG_ABL & 1) {  // timing ablation: no incremental trig
 #pragma unroll
     for (int j = 0; j < 7; ++j) sn[j] += d[j];
@@ -902,7 +1012,7 @@ IKG_HD inline void trig_advance(T qc, const T* qa, const T* q_old, bool resync, 
 // it.  WORLD = true: world frame (collision continuation, which needs world
 // joint frames).  The minimum-norm step is the same in any frame (§3).
 template <typename T, class SP, bool WANT_FRAMES = false, bool WORLD = WANT_FRAMES>
-IKG_HD inline T arm_fk_error(const KModel<T>* __restrict__ m, int arm, const T* sn, const T* cs, const T* RT,
+IKG_HD inline T arm_fk_error(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const T* sn, const T* cs, const T* RT,
                              const T* tT, ArmState<T>& st, T (*frames)[12] = nullptr,
                              ThetaTrack<T>* tk = nullptr, bool resync = true) {
   T Rc[9], tc[3];
@@ -966,7 +1076,7 @@ IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b
   cross3(g3, g1, r2);
   cross3(g1, g2, r3);
   const T det = dot3(g1, r1);
-  const T rdet = det != T(0) ? frcp(det) : T(0);
+  const T rdet = vsel<T>(det != T(0), frcp(det), T(0));
   x0[0] = dot3(r1, b0) * rdet;
   x0[1] = dot3(r2, b0) * rdet;
   x0[2] = dot3(r3, b0) * rdet;
@@ -1093,18 +1203,24 @@ IKG_HD inline void arm_dq_damped(const T (&A)[6][8], const T* ze, const T* zc, T
 
 // pin.integrate (q + dq * DT, :86) then projecttojointlimits (:89).
 template <typename T>
-IKG_HD inline void arm_update(const KModel<T>* __restrict__ m, int arm, T dt, T s, const T* dq, T& qc, T* qa) {
+IKG_HD inline void arm_update(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, T dt, T s, const T* dq, T& qc, T* qa) {
   const bool right = arm != 0;
-  qc = clampq(qc + s * dt, m->root_lo, m->root_hi);
+  qc = clampq(qc + s * dt, T(m->root_lo), T(m->root_hi));
+  if constexpr (is_packed<T>) {  // both arms in the lane: packed limits
 #pragma unroll
-  for (int k = 0; k < kArmDof; ++k) {
-    // clamp against both arms' (scalar) limits and select the result: 2 VALU
-    // ops per bound with scalar operands instead of materialising per-lane
-    // limits (the pair kernel has no registers to keep them)
-    const T v = qa[k] + dq[k] * dt;
-    const T qL = clampq(v, m->arm_lo[0][k], m->arm_hi[0][k]);
-    const T qR = clampq(v, m->arm_lo[1][k], m->arm_hi[1][k]);
-    qa[k] = sel(right, qR, qL);
+    for (int k = 0; k < kArmDof; ++k)
+      qa[k] = clampq(qa[k] + dq[k] * dt, T{m->arm_lo[0][k], m->arm_lo[1][k]}, T{m->arm_hi[0][k], m->arm_hi[1][k]});
+  } else {
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) {
+      // clamp against both arms' (scalar) limits and select the result: 2 VALU
+      // ops per bound with scalar operands instead of materialising per-lane
+      // limits (the pair kernel has no registers to keep them)
+      const T v = qa[k] + dq[k] * dt;
+      const T qL = clampq(v, m->arm_lo[0][k], m->arm_hi[0][k]);
+      const T qR = clampq(v, m->arm_lo[1][k], m->arm_hi[1][k]);
+      qa[k] = sel(right, qR, qL);
+    }
   }
 }
 
@@ -1126,6 +1242,18 @@ IKG_HD inline void hook_target(const KModel<T>* __restrict__ m, int arm, const T
   matvec3(CR, Ht, d);
 #pragma unroll
   for (int i = 0; i < 3; ++i) tT[i] = Ct[i] + d[i];
+}
+
+// Both arms' hook targets in one packed lane (x = left, y = right).
+IKG_HD inline void hook_target_packed(const KModel<float>* __restrict__ m, const float* __restrict__ tg, v2f* RT,
+                                      v2f* tT) {
+  float RL[9], tL[3], RR[9], tR[3];
+  hook_target(m, 0, tg, RL, tL);
+  hook_target(m, 1, tg, RR, tR);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) RT[i] = v2f{RL[i], RR[i]};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) tT[i] = v2f{tL[i], tR[i]};
 }
 
 }  // namespace ikg

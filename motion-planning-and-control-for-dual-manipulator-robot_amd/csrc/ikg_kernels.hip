@@ -20,19 +20,33 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 #include "ikg_device.hpp"
+#include "ikgrasp.h"
 #include "ikg_launch.hpp"
 
 namespace ikg {
 
-// One problem, one arm: run the reference loop to its stop condition.
-// Returns (through refs) the final q of this lane, the update count and the
-// norm of this lane's hand error at the returned q.
+// Stop test of inverse_geometry.py:70 on squared norms (KParams::eps2):
+// pair layout = this lane's hand and the partner's; packed = both halves.
+template <typename T, typename E>
+__device__ inline bool both_below(T x, T xo, E eps2) {
+  if constexpr (is_packed<T>)
+    return all_of(x < T(eps2));
+  else
+    return x < eps2 && xo < eps2;
+}
+
+// One problem: run the reference loop to its stop condition.  T = double /
+// float: this lane owns one arm (pair layout, partner = lane ^ 1); T = v2f:
+// this lane owns both arms (packed layout).  Returns (through refs) the final
+// q of this lane, the update count and the hand error norms at the returned q.
 template <typename T, bool DAMPED, class SP>
-__device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, const T* RT,
-                                  const T* tT, T& qc, T* qa, int& it_out, bool& conv_out, T& nrm_out,
-                                  T& other_out) {
+__device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
+                                  const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
+                                  T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out) {
+  static_assert(!(DAMPED && is_packed<T>), "the packed layout implements lambda = 0 only");
   T sn[7], cs[7];
   trig_exact(qc, qa, sn, cs);
   int it = 0;
@@ -41,7 +55,7 @@ __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams
   ThetaTrack<T> tk{};
   for (;;) {
     ArmState<T> st;
-    if constexpr (IKG_THETA_TRACK && sizeof(T) == 8)  // fp32: atan2f is as cheap (measured)
+    if constexpr (IKG_THETA_TRACK && is_f64<T>)  // fp32: atan2f is as cheap (measured)
       x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, &tk, (it % Trig<T>::kResync) == 0);
     else
       x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
@@ -62,7 +76,7 @@ __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams
     }
     xo = pair_swap(x);
     if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
-    if (x < prm.eps2 && xo < prm.eps2) {  // |e_L| < eps and |e_R| < eps (:70)
+    if (both_below(x, xo, prm.eps2)) {  // |e_L| < eps and |e_R| < eps (:70)
       conv = true;
       break;
     }
@@ -70,7 +84,7 @@ __device__ inline void solve_pair(const KModel<T>* __restrict__ m, const KParams
     q_old[0] = qc;
 #pragma unroll
     for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
-    arm_update(m, arm, prm.dt, s, dq, qc, qa);
+    arm_update(m, arm, T(prm.dt), s, dq, qc, qa);
     ++it;
     trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }
@@ -143,6 +157,51 @@ __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __r
     if (iters_out) iters_out[p] = it;
   }
   if (err_out) err_out[p * 2 + arm] = nrm;
+}
+
+// Packed fp32 layout: one lane per problem, both arms in 2-vectors, so every
+// v_pk_{fma,mul,add}_f32 advances both arms and a wave holds 64 problems
+// (DESIGN.md §3).  Same loop, same arithmetic as the pair kernel's fp32 path.
+template <class SP>
+__global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
+                                                              KParams<float> prm, const float* __restrict__ targets,
+                                                              const float* __restrict__ q0, int64_t q0_stride,
+                                                              int64_t B, int64_t S, float* __restrict__ q_out,
+                                                              uint8_t* __restrict__ conv_out,
+                                                              int32_t* __restrict__ iters_out,
+                                                              float* __restrict__ err_out) {
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= B) return;
+  const int64_t tgt = S > 1 ? p / S : p;
+  const int64_t row = S > 1 ? p - tgt * S : p;
+  v2f RT[9], tT[3];
+  hook_target_packed(m, targets + tgt * 12, RT, tT);
+  const float* qrow = q0 + row * q0_stride;
+  v2f qc = v2f(qrow[m->root_q]), qa[kArmDof];
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) qa[k] = v2f{qrow[m->arm_q[0][k]], qrow[m->arm_q[1][k]]};
+  int it;
+  bool conv;
+  v2f nrm, other;
+  solve_pair<v2f, false, SP>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
+  float* qo = q_out + p * m->nq;
+  qo[m->root_q] = qc.x;
+  for (int i = 0; i < m->n_passive; ++i) {  // moved only by the first update's clamp (tools.py:21-22)
+    const int j = m->passive_q[i];
+    const float v = qrow[j];
+    qo[j] = it > 0 ? clampq(v, m->lo[j], m->hi[j]) : v;
+  }
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) {
+    qo[m->arm_q[0][k]] = qa[k].x;
+    qo[m->arm_q[1][k]] = qa[k].y;
+  }
+  if (conv_out) conv_out[p] = conv ? 1 : 0;
+  if (iters_out) iters_out[p] = it;
+  if (err_out) {
+    err_out[p * 2] = nrm.x;
+    err_out[p * 2 + 1] = nrm.y;
+  }
 }
 
 // Multi-start best-seed reduction: one wave per target reduces the S seed
@@ -281,10 +340,44 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
                      a.iters, (T*)a.err_out);
 }
 
+// The packed layout applies to fp32, the compiled Nextage specialisation and
+// lambda = 0.  It halves the instructions per problem but v_pk_fma_f32 issues
+// at ~4.4 cycles against ~2.7 for v_fma_f32 (tools/ubench/pkl.hip), and it
+// halves the waves: measured faster only once the pair layout would hold >= 2
+// waves per SIMD (B >= 65536 on 256 CUs: -8%, B = 4096: +30%).  AUTO takes it
+// from there on.
+template <typename T>
+bool packed_applies(const KParams<T>& prm, int spec) {
+  return std::is_same<T, float>::value && spec == kSpecNextage && !(prm.lambda > T(0));
+}
+
+static int64_t packed_min_batch() {
+  static int64_t v = -1;
+  if (v < 0) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    v = (int64_t)cus * 4 /* SIMDs */ * 2 /* waves */ * 32 /* problems per pair wave */;
+  }
+  return v;
+}
+
 template <typename T>
 hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,
                              hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
+  if constexpr (std::is_same<T, float>::value) {
+    const bool want = a.variant == IKG_VARIANT_PACKED || (a.variant == IKG_VARIANT_AUTO && a.B >= packed_min_batch());
+    if (want && packed_applies(prm, spec)) {
+      const dim3 grid((unsigned)((a.B + 63) / 64));
+      hipLaunchKernelGGL((ikg_packed_batch_kernel<SpecNextage>), grid, dim3(64), 0, s, dmodel, prm,
+                         (const float*)a.targets, (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out,
+                         a.converged, a.iters, (float*)a.err_out);
+      return hipGetLastError();
+    }
+  }
+  if (a.variant == IKG_VARIANT_PACKED) return hipErrorInvalidValue;  // checked by the C-ABI first
   const bool damped = prm.lambda > T(0);
   if (spec == kSpecNextage) {
     if (damped)
@@ -306,6 +399,7 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   if (a.T <= 0) return hipSuccess;
   // 1) every (target, seed) problem through the pair kernel into the workspace
   BatchArgs b{a.targets, a.seeds, a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
+  b.variant = a.variant;
   hipError_t e = launch_pair_batch<T>(dmodel, prm, b, spec, s);
   if (e != hipSuccess) return e;
   if (a.collision) {  // converged-but-colliding seeds keep iterating (inverse_geometry.py:70)

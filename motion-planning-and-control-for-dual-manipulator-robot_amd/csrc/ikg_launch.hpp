@@ -20,6 +20,7 @@ struct BatchArgs {
   void* err_out;
   int ppw;         // problems per 64-lane wave (1..32)
   int64_t S = 1;   // seeds per target (multi-start): problem p = (target p / S, q0 row p % S)
+  int variant = 0; // ikg_variant
 };
 
 struct MultiArgs {
@@ -42,6 +43,7 @@ struct MultiArgs {
   // go through the collision continuation before the best-seed reduction
   const void* collision = nullptr;
   int n_geoms = 0;
+  int variant = 0;  // ikg_variant of the per-seed solves
 };
 
 // kernel specialisation chosen at model creation (ikg_model_build.hpp)

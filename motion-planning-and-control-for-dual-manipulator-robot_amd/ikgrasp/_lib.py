@@ -16,7 +16,7 @@ IKG_MAX_PAIRS = 1024
 IKG_ARM_DOF = 6
 IKG_F64, IKG_F32 = 0, 1
 IKG_FLAG_HOST_POINTERS = 1
-IKG_VARIANT_AUTO, IKG_VARIANT_PAIR, IKG_VARIANT_WAVE = 0, 1, 2
+IKG_VARIANT_AUTO, IKG_VARIANT_PAIR, IKG_VARIANT_PACKED = 0, 1, 2
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("IKGRASP_LIB", os.path.join(_HERE, "_native", "libikgrasp.so"))

@@ -230,3 +230,47 @@ def test_problems_per_wave_does_not_change_results(solver):
     for ppw in (1, 3, 4, 16):
         s = solver.solve(tg, np.zeros(15), ppw=ppw)
         assert np.array_equal(s.q, ref.q) and np.array_equal(s.iters, ref.iters) and np.array_equal(s.err, ref.err)
+
+
+# ---------------------------------------------------------------- packed fp32 layout (IKG_VARIANT_PACKED)
+@pytest.mark.parametrize("variant", [1, 2])  # PAIR, PACKED
+def test_fixture_parity_fp32_layouts(solver, oracle_cases, variant):
+    c = oracle_cases
+    sol = solver.solve(c["targets"], c["q0"], dtype="f32", variant=variant)
+    conv = c["converged"] & sol.converged
+    assert np.array_equal(sol.converged, c["converged"])
+    assert np.abs(sol.iters[conv].astype(int) - c["iters"][conv]).max() <= 2
+    hands_gpu = solver.fk(sol.q.astype(np.float64))
+    hands_orc = solver.fk(c["q"])
+    for h in range(2):
+        e = helpers.se3_err(hands_orc[conv, h, :9].reshape(-1, 3, 3), hands_orc[conv, h, 9:],
+                            hands_gpu[conv, h, :9].reshape(-1, 3, 3), hands_gpu[conv, h, 9:])
+        assert e.max() <= 1e-4
+    _check_reported_errors(solver, sol, c["targets"], 2e-5)
+
+
+def test_packed_layout_matches_pair_layout_at_scale(solver):
+    # same fp32 arithmetic in a different lane layout: identical up to the
+    # scheduling of the packed instructions (flags and iteration counts
+    # identical for >= 99.5%, end effectors within the fp32 tolerance)
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(8192, seed=11)
+    a = solver.solve(tg, np.zeros(15), dtype="f32", variant=1)
+    b = solver.solve(tg, np.zeros(15), dtype="f32", variant=2)
+    assert (a.converged == b.converged).mean() >= 0.995
+    both = a.converged & b.converged
+    assert (a.iters[both] == b.iters[both]).mean() >= 0.99
+    ha, hb = solver.fk(a.q.astype(np.float64)), solver.fk(b.q.astype(np.float64))
+    for h in range(2):
+        e = helpers.se3_err(ha[both, h, :9].reshape(-1, 3, 3), ha[both, h, 9:],
+                            hb[both, h, :9].reshape(-1, 3, 3), hb[both, h, 9:])
+        assert e.max() <= 1e-4
+
+
+def test_packed_variant_rejected_where_it_does_not_apply(solver, kat):
+    from ikgrasp._lib import IkgError
+    tg = np.stack([_placement_row(kat["cube_placement"])])
+    with pytest.raises(IkgError):
+        solver.solve(tg, np.zeros(15), dtype="f64", variant=2)
+    with pytest.raises(IkgError):
+        solver.solve(tg, np.zeros(15), dtype="f32", variant=2, lam=1e-3)

@@ -38,7 +38,8 @@ for p in libs:
     h = C.c_void_p()
     assert lib.ikg_model_create(C.byref(desc), C.byref(h)) == 0
     handles.append((os.path.relpath(p, ROOT)[-40:], lib, h))
-prm = _lib.Params(eps=float(os.environ.get("ABL_EPS", "1e-37")), dt=1e-2, max_iters=1000, variant=0, lambda_=0.0)
+prm = _lib.Params(eps=float(os.environ.get("ABL_EPS", "1e-37")), dt=1e-2, max_iters=1000,
+                  variant=int(os.environ.get("ABL_VARIANT", "0")), lambda_=0.0)
 s = torch.cuda.current_stream().cuda_stream
 times = {n: [] for n, _, _ in handles}
 for rnd in range(6):
