@@ -176,6 +176,29 @@ int ikg_log6_batch(int device, int dtype, const void* M, int64_t B, void* out, v
 int ikg_collision_batch(const ikg_model* model, int device, int dtype, const void* q, const void* targets,
                         int64_t B, uint8_t* in_collision, void* stream, uint32_t flags);
 
+/*
+ * Batched distance query, tools.distanceToObstacle(robot, q) (tools.py:37-51):
+ * the minimum over the active pairs listed in pair_idx (indices into the
+ * scene's pair list; the reference takes the pairs whose second geometry is
+ * the table or the obstacle) of the pair distance (hpp-fcl
+ * computeDistance().min_distance; <= 0 when the pair intersects):
+ *   q [B,nq], targets [B,12] -> dist [B].  pair_idx is a host array.
+ */
+int ikg_distance_batch(const ikg_model* model, int device, int dtype, const void* q, const void* targets,
+                       int64_t B, const int32_t* pair_idx, int32_t n_pairs, void* dist, void* stream,
+                       uint32_t flags);
+
+/*
+ * Batched cube-placement check of the planner's sampler / path projection
+ * (path.py:51-52, :136-138: pin.computeCollisions on the cube's own collision
+ * model, setup_pinocchio.py:62-70): the scene's target geometry placed at each
+ * targets[i] against the world-fixed geometries listed in geoms (host array):
+ *   targets [B,12] -> in_collision [B].
+ */
+int ikg_target_env_batch(const ikg_model* model, int device, int dtype, const void* targets, int64_t B,
+                         const int32_t* geoms, int32_t n_geoms, uint8_t* in_collision, void* stream,
+                         uint32_t flags);
+
 /* Thread-local message of the last failure ("" if none). */
 const char* ikg_last_error(void);
 

@@ -601,3 +601,107 @@ int ikg_collision_batch(const ikg_model* model, int device, int dtype, const voi
 }
 
 }  // extern "C"
+
+// Small index arrays of the planner queries: host -> device each call.
+template <typename T>
+int distance_t(ikg_model* model, int device, const void* q, const void* targets, int64_t B, const int32_t* idx,
+               int32_t n, void* out, hipStream_t s, uint32_t flags) {
+  const ikg::KModel<T>* dm = nullptr;
+  const ikg::KCollision<T>* dc = nullptr;
+  int rc = model->device_tables<T>(device, &dm);
+  if (rc || (rc = model->collision_tables<T>(device, &dc))) return rc;
+  const int nq = model->desc.nq;
+  Staging st(s);
+  const bool host = flags & IKG_FLAG_HOST_POINTERS;
+  const void* dq = q;
+  const void* dt = targets;
+  void* dout = out;
+  const int32_t* didx = (const int32_t*)st.in(idx, sizeof(int32_t) * n);
+  if (host) {
+    dq = st.in(q, sizeof(T) * nq * B);
+    dt = st.in(targets, sizeof(T) * 12 * B);
+    dout = st.out(sizeof(T) * B);
+  }
+  if (st.rc) return st.rc;
+  hipError_t e = ikg::launch_distance<T>(dm, dc, dq, dt, B, didx, n, dout, s);
+  if (e != hipSuccess) return hip_fail(e, "ikg distance kernel launch");
+  if (host) st.back(out, dout, sizeof(T) * B);
+  if (st.rc) return st.rc;
+  e = hipStreamSynchronize(s);  // the staged index array is freed on return
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return IKG_OK;
+}
+
+template <typename T>
+int target_env_t(ikg_model* model, int device, const void* targets, int64_t B, const int32_t* geoms, int32_t n,
+                 uint8_t* out, hipStream_t s, uint32_t flags) {
+  const ikg::KCollision<T>* dc = nullptr;
+  int rc = model->collision_tables<T>(device, &dc);
+  if (rc) return rc;
+  Staging st(s);
+  const bool host = flags & IKG_FLAG_HOST_POINTERS;
+  const void* dt = targets;
+  uint8_t* dout = out;
+  const int32_t* dg = (const int32_t*)st.in(geoms, sizeof(int32_t) * n);
+  if (host) {
+    dt = st.in(targets, sizeof(T) * 12 * B);
+    dout = (uint8_t*)st.out(B);
+  }
+  if (st.rc) return st.rc;
+  hipError_t e = ikg::launch_target_env<T>(dc, dt, B, dg, n, dout, s);
+  if (e != hipSuccess) return hip_fail(e, "ikg target/env kernel launch");
+  if (host) st.back(out, dout, B);
+  if (st.rc) return st.rc;
+  e = hipStreamSynchronize(s);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  return IKG_OK;
+}
+
+extern "C" {
+
+int ikg_distance_batch(const ikg_model* model, int device, int dtype, const void* q, const void* targets,
+                       int64_t B, const int32_t* pair_idx, int32_t n_pairs, void* dist, void* stream,
+                       uint32_t flags) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (B < 0) return fail(IKG_EINVAL, "B must be >= 0");
+  if (n_pairs < 1 || !pair_idx) return fail(IKG_EINVAL, "pair_idx must list at least one pair");
+  if (B > 0 && (!q || !targets || !dist)) return fail(IKG_EINVAL, "q, targets and dist are required");
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  if (!model->has_collision) return fail(IKG_EINVAL, "no collision scene attached (ikg_model_set_collision)");
+  for (int32_t k = 0; k < n_pairs; ++k)
+    if (pair_idx[k] < 0 || pair_idx[k] >= model->c64.n_pairs)
+      return fail(IKG_EINVAL, "pair_idx[%d] = %d outside [0, %d)", k, pair_idx[k], model->c64.n_pairs);
+  if (B > 0x7fffffff) return fail(IKG_EINVAL, "B too large for one launch");
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  if (B == 0) return IKG_OK;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == IKG_F64 ? distance_t<double>(m, device, q, targets, B, pair_idx, n_pairs, dist, s, flags)
+                          : distance_t<float>(m, device, q, targets, B, pair_idx, n_pairs, dist, s, flags);
+}
+
+int ikg_target_env_batch(const ikg_model* model, int device, int dtype, const void* targets, int64_t B,
+                         const int32_t* geoms, int32_t n_geoms, uint8_t* in_collision, void* stream,
+                         uint32_t flags) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (B < 0) return fail(IKG_EINVAL, "B must be >= 0");
+  if (n_geoms < 1 || !geoms) return fail(IKG_EINVAL, "geoms must list at least one geometry");
+  if (B > 0 && (!targets || !in_collision)) return fail(IKG_EINVAL, "targets and in_collision are required");
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  if (!model->has_collision) return fail(IKG_EINVAL, "no collision scene attached (ikg_model_set_collision)");
+  for (int32_t k = 0; k < n_geoms; ++k)
+    if (geoms[k] < 0 || geoms[k] >= model->c64.n_geoms || geoms[k] == model->c64.target_geom)
+      return fail(IKG_EINVAL, "geoms[%d] = %d is not a scene geometry other than the target", k, geoms[k]);
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  if (B == 0) return IKG_OK;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == IKG_F64 ? target_env_t<double>(m, device, targets, B, geoms, n_geoms, in_collision, s, flags)
+                          : target_env_t<float>(m, device, targets, B, geoms, n_geoms, in_collision, s, flags);
+}
+
+}  // extern "C"

@@ -159,6 +159,99 @@ __global__ __launch_bounds__(64) void ikg_collision_kernel(const KModel<T>* __re
   if (lane == 0) out[p] = col ? 1 : 0;
 }
 
+// ---------------------------------------------------------------- planner queries
+// distanceToObstacle (tools.py:37-51): min over the given active pairs of the
+// pair distance at configuration q, one wave per configuration.
+template <typename T>
+__global__ __launch_bounds__(64) void ikg_distance_kernel(const KModel<T>* __restrict__ m,
+                                                          const KCollision<T>* __restrict__ c,
+                                                          const T* __restrict__ q, const T* __restrict__ targets,
+                                                          int64_t B, const int32_t* __restrict__ pair_idx, int n_idx,
+                                                          T* __restrict__ out) {
+  __shared__ CollideScratch<T> S;
+  __shared__ T tgt[12];
+  const int64_t p = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (lane < m->nq) S.q[lane] = q[p * m->nq + lane];
+  if (lane < 12) tgt[lane] = targets[p * 12 + lane];
+  __syncthreads();
+  stage_trig_par(m, S);
+  __syncthreads();
+  if (lane < m->nq) joint_local(m, lane, S.sn[lane], S.cs[lane], S.L[lane]);
+  __syncthreads();
+  if (lane < m->nq) joint_world(S.par, lane, S.L, S.F[lane]);
+  __syncthreads();
+  for (int g = lane; g < c->n_geoms; g += 64) geom_world(c, g, S.F, tgt, S.P[g]);
+  __syncthreads();
+  // GJK in fp64 whatever the I/O type: the fp32 rounding of the simplex tests
+  // (flat tetrahedra against the table's faces) is not worth a separate tuning
+  double d = 1e30;
+  for (int k = lane; k < n_idx; k += 64) {
+    const int pr = pair_idx[k];
+    double P2[2][12], D2[2][3];
+    int K2[2];
+    for (int h = 0; h < 2; ++h) {
+      const int g = c->pairs[pr][h];
+      for (int i = 0; i < 12; ++i) P2[h][i] = (double)S.P[g][i];
+      for (int i = 0; i < 3; ++i) D2[h][i] = (double)c->dims[g][i];
+      K2[h] = c->kind[g];
+    }
+    const Shape<double> A{P2[0], P2[0] + 9, D2[0], K2[0]}, Bs{P2[1], P2[1] + 9, D2[1], K2[1]};
+    d = fmin(d, pair_distance(A, Bs));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) d = fmin(d, __shfl_xor(d, off));
+  if (lane == 0) out[p] = (T)d;
+}
+
+// The cube's own collision model (setup_pinocchio.py:62-70): the target
+// geometry placed at each candidate placement against the given world-fixed
+// geometries (table, obstacle), one thread per placement.
+template <typename T>
+__global__ __launch_bounds__(256) void ikg_target_env_kernel(const KCollision<T>* __restrict__ c,
+                                                             const T* __restrict__ targets, int64_t B,
+                                                             const int32_t* __restrict__ geoms, int n_geoms,
+                                                             uint8_t* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const T* P = targets + 12 * i;
+  const int tg = c->target_geom;
+  const Shape<T> A{P, P + 9, c->dims[tg], c->kind[tg]};
+  int hit = 0;
+  for (int k = 0; k < n_geoms; ++k) {
+    const int g = geoms[k];
+    const Shape<T> Bs{c->R[g], c->t[g], c->dims[g], c->kind[g]};
+    hit |= pair_collides(A, Bs) != 0;
+  }
+  out[i] = hit ? 1 : 0;
+}
+
+template <typename T>
+hipError_t launch_distance(const KModel<T>* dm, const KCollision<T>* dc, const void* q, const void* targets,
+                           int64_t B, const int32_t* pair_idx, int n_idx, void* out, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL((ikg_distance_kernel<T>), dim3((unsigned)B), dim3(64), 0, s, dm, dc, (const T*)q,
+                     (const T*)targets, B, pair_idx, n_idx, (T*)out);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_target_env(const KCollision<T>* dc, const void* targets, int64_t B, const int32_t* geoms,
+                             int n_geoms, uint8_t* out, hipStream_t s) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL((ikg_target_env_kernel<T>), dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, dc,
+                     (const T*)targets, B, geoms, n_geoms, out);
+  return hipGetLastError();
+}
+template hipError_t launch_distance<double>(const KModel<double>*, const KCollision<double>*, const void*,
+                                            const void*, int64_t, const int32_t*, int, void*, hipStream_t);
+template hipError_t launch_distance<float>(const KModel<float>*, const KCollision<float>*, const void*,
+                                           const void*, int64_t, const int32_t*, int, void*, hipStream_t);
+template hipError_t launch_target_env<double>(const KCollision<double>*, const void*, int64_t, const int32_t*, int,
+                                              uint8_t*, hipStream_t);
+template hipError_t launch_target_env<float>(const KCollision<float>*, const void*, int64_t, const int32_t*, int,
+                                             uint8_t*, hipStream_t);
+
 // ---------------------------------------------------------------- continuation
 // G problems per wave (LG = 64/G lanes each).  Per-problem state lives in a
 // slice of dynamic LDS sized for the model (group_lds_bytes).

@@ -295,6 +295,271 @@ IKG_HD inline int pair_collides(const Shape<T>& A, const Shape<T>& B, T* cert = 
   return gjk_intersect(A, B, cert);
 }
 
+// ---------------------------------------------------------------- distance
+// hpp-fcl computeDistance().min_distance for one pair (tools.py:37-51,
+// distanceToObstacle): the Euclidean distance between two separated convex
+// shapes.  Spheres are handled as their centre point (radius subtracted at
+// the end), a sphere against a box exactly; everything else by GJK with the
+// closest point of the simplex computed by Voronoi-region tests (Ericson,
+// Real-Time Collision Detection §5.1).  Returns <= 0 when the shapes
+// intersect (the reference only queries collision-free configurations).
+template <typename T>
+struct DSimplex {
+  T w[4][3];
+  int n;
+};
+
+// Closest point to the origin of segment [a, b]; keeps the supporting subset.
+template <typename T>
+IKG_HD inline void closest_seg(DSimplex<T>& S, T* v) {
+  const T* a = S.w[0];
+  const T* b = S.w[1];
+  T ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  const T t = -dot3(a, ab);
+  const T l2 = dot3(ab, ab);
+  if (t <= T(0) || l2 <= T(0)) {
+    S.n = 1;
+    cp3(v, a);
+    return;
+  }
+  if (t >= l2) {
+    S.n = 1;
+    cp3(S.w[0], b);
+    cp3(v, b);
+    return;
+  }
+  const T u = t / l2;
+  for (int i = 0; i < 3; ++i) v[i] = a[i] + u * ab[i];
+}
+
+// Closest point to the origin of segment [a, b] (no simplex bookkeeping).
+template <typename T>
+IKG_HD inline void seg_point(const T* a, const T* b, T* v, T& t_out) {
+  T ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+  const T l2 = dot3(ab, ab);
+  T t = l2 > T(0) ? -dot3(a, ab) / l2 : T(0);
+  t = fmin(fmax(t, T(0)), T(1));
+  t_out = t;
+  for (int i = 0; i < 3; ++i) v[i] = a[i] + t * ab[i];
+}
+
+// Closest point to the origin of triangle (a, b, c) (Ericson 5.1.5, p = 0);
+// region: 0/1/2 vertex a/b/c, 3 edge ab, 4 edge ac, 5 edge bc, 6 face.  A
+// degenerate (zero-area) triangle resolves to the closest of its edges.
+template <typename T>
+IKG_HD inline void closest_tri(const T* a, const T* b, const T* c, T* v, int& region) {
+  T ab[3], ac[3], ap[3];
+  for (int i = 0; i < 3; ++i) {
+    ab[i] = b[i] - a[i];
+    ac[i] = c[i] - a[i];
+    ap[i] = -a[i];
+  }
+  T n[3];
+  cross3(ab, ac, n);
+  const T scale = dot3(ab, ab) * dot3(ac, ac);
+  if (!(dot3(n, n) > T(1e-24) * scale)) {  // degenerate: best edge
+    T v1[3], v2[3], v3[3], t1, t2, t3;
+    seg_point(a, b, v1, t1);
+    seg_point(a, c, v2, t2);
+    seg_point(b, c, v3, t3);
+    const T d1 = dot3(v1, v1), d2 = dot3(v2, v2), d3 = dot3(v3, v3);
+    if (d1 <= d2 && d1 <= d3) {
+      cp3(v, v1);
+      region = t1 <= T(0) ? 0 : (t1 >= T(1) ? 1 : 3);
+    } else if (d2 <= d3) {
+      cp3(v, v2);
+      region = t2 <= T(0) ? 0 : (t2 >= T(1) ? 2 : 4);
+    } else {
+      cp3(v, v3);
+      region = t3 <= T(0) ? 1 : (t3 >= T(1) ? 2 : 5);
+    }
+    return;
+  }
+  const T d1 = dot3(ab, ap), d2 = dot3(ac, ap);
+  if (d1 <= T(0) && d2 <= T(0)) {
+    region = 0;
+    cp3(v, a);
+    return;
+  }
+  T bp[3] = {-b[0], -b[1], -b[2]};
+  const T d3 = dot3(ab, bp), d4 = dot3(ac, bp);
+  if (d3 >= T(0) && d4 <= d3) {
+    region = 1;
+    cp3(v, b);
+    return;
+  }
+  const T vc = d1 * d4 - d3 * d2;
+  if (vc <= T(0) && d1 >= T(0) && d3 <= T(0)) {
+    const T u = d1 / (d1 - d3);
+    region = 3;
+    for (int i = 0; i < 3; ++i) v[i] = a[i] + u * ab[i];
+    return;
+  }
+  T cpn[3] = {-c[0], -c[1], -c[2]};
+  const T d5 = dot3(ab, cpn), d6 = dot3(ac, cpn);
+  if (d6 >= T(0) && d5 <= d6) {
+    region = 2;
+    cp3(v, c);
+    return;
+  }
+  const T vb = d5 * d2 - d1 * d6;
+  if (vb <= T(0) && d2 >= T(0) && d6 <= T(0)) {
+    const T w_ = d2 / (d2 - d6);
+    region = 4;
+    for (int i = 0; i < 3; ++i) v[i] = a[i] + w_ * ac[i];
+    return;
+  }
+  const T va = d3 * d6 - d5 * d4;
+  if (va <= T(0) && (d4 - d3) >= T(0) && (d5 - d6) >= T(0)) {
+    const T w_ = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+    region = 5;
+    for (int i = 0; i < 3; ++i) v[i] = b[i] + w_ * (c[i] - b[i]);
+    return;
+  }
+  const T den = T(1) / (va + vb + vc);
+  const T u = vb * den, w_ = vc * den;
+  region = 6;
+  for (int i = 0; i < 3; ++i) v[i] = a[i] + ab[i] * u + ac[i] * w_;
+}
+
+// Reduce S (a triangle, w[0..2]) to the supporting feature of its closest point.
+template <typename T>
+IKG_HD inline void closest_tri_reduce(DSimplex<T>& S, T* v) {
+  int region = 6;
+  closest_tri(S.w[0], S.w[1], S.w[2], v, region);
+  switch (region) {
+    case 0: S.n = 1; break;
+    case 1: S.n = 1; cp3(S.w[0], S.w[1]); break;
+    case 2: S.n = 1; cp3(S.w[0], S.w[2]); break;
+    case 3: S.n = 2; break;
+    case 4: S.n = 2; cp3(S.w[1], S.w[2]); break;
+    case 5: S.n = 2; cp3(S.w[0], S.w[2]); break;  // (c, b)
+    default: S.n = 3; break;
+  }
+}
+
+// Tetrahedron w[0..3]: origin inside -> intersecting (returns true);
+// otherwise the closest point over its faces (all four when the tetrahedron
+// is flat, e.g. a triangle extended by a coplanar box corner; else those
+// facing the origin), reduced to that face's supporting feature.
+template <typename T>
+IKG_HD inline bool closest_tet_reduce(DSimplex<T>& S, T* v) {
+  const int face[4][4] = {{0, 1, 2, 3}, {0, 2, 3, 1}, {0, 3, 1, 2}, {1, 3, 2, 0}};  // 3 verts + opposite
+  T e1[3], e2[3], e3[3], cr[3];
+  for (int i = 0; i < 3; ++i) {
+    e1[i] = S.w[1][i] - S.w[0][i];
+    e2[i] = S.w[2][i] - S.w[0][i];
+    e3[i] = S.w[3][i] - S.w[0][i];
+  }
+  cross3(e2, e3, cr);
+  const T vol = dot3(e1, cr);
+  const T l = fmax(fmax(dot3(e1, e1), dot3(e2, e2)), dot3(e3, e3));
+  const bool flat = !(vol * vol > T(1e-24) * l * l * l);
+  bool inside = !flat;
+  T best = T(0);
+  int best_f = -1;
+  for (int f = 0; f < 4; ++f) {
+    const T* a = S.w[face[f][0]];
+    const T* b = S.w[face[f][1]];
+    const T* c = S.w[face[f][2]];
+    const T* d = S.w[face[f][3]];
+    if (!flat) {
+      T ab[3], ac[3], n[3];
+      for (int i = 0; i < 3; ++i) {
+        ab[i] = b[i] - a[i];
+        ac[i] = c[i] - a[i];
+      }
+      cross3(ab, ac, n);
+      T ad[3] = {d[0] - a[0], d[1] - a[1], d[2] - a[2]};
+      const T sd = dot3(n, ad);  // opposite vertex side
+      const T so = -dot3(n, a);  // origin side
+      if (so * sd >= T(0)) continue;  // origin on the inner side of this face
+      inside = false;
+    }
+    T fv[3];
+    int region = 6;
+    closest_tri(a, b, c, fv, region);
+    const T d2 = dot3(fv, fv);
+    if (best_f < 0 || d2 < best) {
+      best = d2;
+      best_f = f;
+    }
+  }
+  if (inside) return true;
+  T a[3], b[3], c[3];
+  cp3(a, S.w[face[best_f][0]]);
+  cp3(b, S.w[face[best_f][1]]);
+  cp3(c, S.w[face[best_f][2]]);
+  cp3(S.w[0], a);
+  cp3(S.w[1], b);
+  cp3(S.w[2], c);
+  S.n = 3;
+  closest_tri_reduce(S, v);
+  return false;
+}
+
+template <typename T>
+IKG_HD inline T gjk_distance_raw(const Shape<T>& A, const Shape<T>& B) {
+  DSimplex<T> S;
+  T v[3] = {A.t[0] - B.t[0], A.t[1] - B.t[1], A.t[2] - B.t[2]};
+  if (dot3(v, v) == T(0)) v[0] = T(1);
+  {
+    T d[3] = {-v[0], -v[1], -v[2]};
+    mink_support(A, B, d, S.w[0]);
+  }
+  S.n = 1;
+  cp3(v, S.w[0]);
+  const T eps_rel = sizeof(T) == 8 ? T(1e-12) : T(1e-6);
+  for (int it = 0; it < 64; ++it) {
+    const T vv = dot3(v, v);
+    if (vv <= (sizeof(T) == 8 ? T(1e-30) : T(1e-14))) return T(0);  // origin on the simplex: touching
+    T d[3] = {-v[0], -v[1], -v[2]}, w[3];
+    mink_support(A, B, d, w);
+    if (vv - dot3(v, w) <= eps_rel * vv) break;  // no progress towards the origin: |v| is the distance
+    // the new point is never already in the simplex once it made progress
+    cp3(S.w[S.n == 1 ? 1 : (S.n == 2 ? 2 : 3)], w);
+    S.n += 1;
+    T vn[3];
+    if (S.n == 2) {
+      closest_seg(S, vn);
+    } else if (S.n == 3) {
+      closest_tri_reduce(S, vn);
+    } else if (closest_tet_reduce(S, vn)) {
+      return T(0);  // origin inside: intersecting
+    }
+    if (!(dot3(vn, vn) < vv)) break;  // rounding stall: keep the best point found
+    cp3(v, vn);
+  }
+  return sqrt(dot3(v, v));
+}
+
+// distance of one pair (min_distance of hpp-fcl's DistanceResult)
+template <typename T>
+IKG_HD inline T pair_distance(const Shape<T>& A, const Shape<T>& B) {
+  if (A.kind == kSphere && B.kind == kSphere) {
+    T d[3] = {A.t[0] - B.t[0], A.t[1] - B.t[1], A.t[2] - B.t[2]};
+    return sqrt(dot3(d, d)) - A.dims[0] - B.dims[0];
+  }
+  if ((A.kind == kSphere) != (B.kind == kSphere)) {
+    const Shape<T>& Sp = A.kind == kSphere ? A : B;
+    const Shape<T>& X = A.kind == kSphere ? B : A;
+    if (X.kind == kBox || X.kind == kMeshBox) {  // exact: closest point on the box
+      T d[3] = {Sp.t[0] - X.t[0], Sp.t[1] - X.t[1], Sp.t[2] - X.t[2]}, p[3];
+      matvec3_t(X.R, d, p);
+      T e2 = T(0);
+      for (int i = 0; i < 3; ++i) {
+        const T c = fmin(fmax(p[i], -X.dims[i]), X.dims[i]);
+        e2 += (p[i] - c) * (p[i] - c);
+      }
+      return sqrt(e2) - Sp.dims[0];
+    }
+    const T zero[3] = {T(0), T(0), T(0)};
+    const Shape<T> P{Sp.R, Sp.t, zero, kSphere};  // the centre: a sphere of radius 0
+    return gjk_distance_raw(P, X) - Sp.dims[0];
+  }
+  return gjk_distance_raw(A, B);
+}
+
 // ---------------------------------------------------------------- check stages
 // The stages of one check, shared by the wave-parallel driver (collide_wave,
 // ikg_collision.hip) and the host emulator.  Frames are [R(9) row-major, t(3)].

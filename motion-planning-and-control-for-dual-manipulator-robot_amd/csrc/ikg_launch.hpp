@@ -78,4 +78,13 @@ template <typename T>
 hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
                                    const BatchArgs& a, int spec, int nq, int ng, hipStream_t s);
 
+// planner queries: distance over a pair subset; target geometry
+// against world-fixed geometries
+template <typename T>
+hipError_t launch_distance(const KModel<T>* dm, const KCollision<T>* dc, const void* q, const void* targets,
+                           int64_t B, const int32_t* pair_idx, int n_idx, void* out, hipStream_t s);
+template <typename T>
+hipError_t launch_target_env(const KCollision<T>* dc, const void* targets, int64_t B, const int32_t* geoms,
+                             int n_geoms, uint8_t* out, hipStream_t s);
+
 }  // namespace ikg

@@ -75,7 +75,7 @@ class CollisionDesc(C.Structure):
 EXPORTS = [
     "ikg_model_create", "ikg_model_destroy", "ikg_params_default", "ikg_solve_batch",
     "ikg_solve_multistart", "ikg_fk_batch", "ikg_log6_batch", "ikg_last_error", "ikg_version",
-    "ikg_model_set_collision", "ikg_collision_batch",
+    "ikg_model_set_collision", "ikg_collision_batch", "ikg_distance_batch", "ikg_target_env_batch",
 ]
 
 _lib = None
@@ -115,6 +115,10 @@ def load() -> C.CDLL:
     lib.ikg_model_set_collision.restype = i32
     lib.ikg_collision_batch.argtypes = [vp, i32, i32, vp, vp, i64, vp, vp, C.c_uint32]
     lib.ikg_collision_batch.restype = i32
+    lib.ikg_distance_batch.argtypes = [vp, i32, i32, vp, vp, i64, vp, C.c_int32, vp, vp, C.c_uint32]
+    lib.ikg_distance_batch.restype = i32
+    lib.ikg_target_env_batch.argtypes = [vp, i32, i32, vp, i64, vp, C.c_int32, vp, vp, C.c_uint32]
+    lib.ikg_target_env_batch.restype = i32
     lib.ikg_last_error.argtypes = []
     lib.ikg_last_error.restype = C.c_char_p
     lib.ikg_version.argtypes = []

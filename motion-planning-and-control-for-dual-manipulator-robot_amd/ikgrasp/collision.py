@@ -64,6 +64,22 @@ class CollisionScene:
             "pairs": self.pairs.tolist(),
         }, indent=1)
 
+    def geom_id(self, name: str) -> int:
+        """robot.collision_model.getGeometryId(name)"""
+        for i, g in enumerate(self.geoms):
+            if g.name == name:
+                return i
+        raise KeyError(name)
+
+    def obstacle_pairs(self, obstacle="obstaclebase_0", table="baseLink_0") -> np.ndarray:
+        """tools.py:39-41: active pairs whose second geometry is the obstacle or the table."""
+        ids = {self.geom_id(obstacle), self.geom_id(table)}
+        return np.array([k for k, (_, j) in enumerate(self.pairs) if int(j) in ids], dtype=np.int32)
+
+    def env_geoms(self, table="baseLink_0", obstacle="obstaclebase_0") -> np.ndarray:
+        """The cube's collision model partners (setup_pinocchio.py:62-70): table, obstacle."""
+        return np.array([self.geom_id(table), self.geom_id(obstacle)], dtype=np.int32)
+
     @staticmethod
     def from_json(text: str) -> "CollisionScene":
         d = json.loads(text)

@@ -21,6 +21,11 @@ class SE3:
     def Identity() -> "SE3":
         return SE3()
 
+    @staticmethod
+    def Interpolate(A, B, alpha: float) -> "SE3":
+        """pin.SE3.Interpolate"""
+        return interpolate(A, B, alpha)
+
     def __mul__(self, other: "SE3") -> "SE3":
         return SE3(self.rotation @ other.rotation, self.translation + self.rotation @ other.translation)
 
@@ -40,6 +45,63 @@ class SE3:
 
     def __repr__(self) -> str:
         return f"SE3(R={self.rotation.tolist()}, p={self.translation.tolist()})"
+
+
+def _skew(w):
+    return np.array([[0.0, -w[2], w[1]], [w[2], 0.0, -w[0]], [-w[1], w[0], 0.0]])
+
+
+_PREC3 = np.finfo(np.float64).eps ** 0.25  # Pinocchio TaylorSeriesExpansion::precision<3>()
+
+
+def log6(M) -> np.ndarray:
+    """pin.log6 -> [v; w] (host-side, for placement interpolation; the IK's
+    log6 runs in the kernel)."""
+    R, p = as_rt(M)
+    tr = R[0, 0] + R[1, 1] + R[2, 2]
+    theta = 0.0 if tr > 3.0 else (math.pi if tr < -1.0 else math.acos((tr - 1.0) / 2.0))
+    if theta >= math.pi - 1e-2:
+        cphi = math.cos(theta - math.pi)
+        beta = theta * theta / (1.0 + cphi)
+        tmp = (np.diag(R) + cphi) * beta
+        sgn = np.where([R[2, 1] > R[1, 2], R[0, 2] > R[2, 0], R[1, 0] > R[0, 1]], 1.0, -1.0)
+        w = sgn * np.sqrt(np.maximum(tmp, 0.0))
+    else:
+        f = theta / math.sin(theta) if theta > _PREC3 else 1.0
+        w = 0.5 * f * np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+    t2 = theta * theta
+    if theta < _PREC3:
+        alpha, beta = 1.0 - t2 / 12.0 - t2 * t2 / 720.0, 1.0 / 12.0 + t2 / 720.0
+    else:
+        st, ct = math.sin(theta), math.cos(theta)
+        alpha = theta * st / (2.0 * (1.0 - ct))
+        beta = 1.0 / t2 - st / (2.0 * theta * (1.0 - ct))
+    v = alpha * p - 0.5 * np.cross(w, p) + (beta * np.dot(w, p)) * w
+    return np.concatenate([v, w])
+
+
+def exp6(v) -> "SE3":
+    """pin.exp6 of [v; w]."""
+    lin, w = np.asarray(v[:3], dtype=np.float64), np.asarray(v[3:], dtype=np.float64)
+    t2 = float(w @ w)
+    t = math.sqrt(t2)
+    if t < _PREC3:
+        a, b, c = 1.0 - t2 / 6.0, 0.5 - t2 / 24.0, 1.0 / 6.0 - t2 / 120.0
+    else:
+        st, ct = math.sin(t), math.cos(t)
+        a, b, c = st / t, (1.0 - ct) / t2, (t - st) / (t2 * t)
+    W = _skew(w)
+    WW = W @ W
+    return SE3(np.eye(3) + a * W + b * WW, (np.eye(3) + b * W + c * WW) @ lin)
+
+
+def interpolate(A, B, alpha: float) -> "SE3":
+    """pin.SE3.Interpolate(A, B, alpha) = A * exp6(alpha * log6(A^-1 B))
+    (path.py:141)."""
+    Ra, ta = as_rt(A)
+    Rb, tb = as_rt(B)
+    a = SE3(Ra, ta)
+    return a * exp6(alpha * log6(a.inverse() * SE3(Rb, tb)))
 
 
 def rotate(axis: str, angle: float) -> np.ndarray:

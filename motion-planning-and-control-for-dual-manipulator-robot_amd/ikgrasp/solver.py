@@ -195,6 +195,37 @@ class IKSolver:
                                                 qq.shape[0], out.ctypes.data, None, _lib.IKG_FLAG_HOST_POINTERS))
         return out.astype(bool)
 
+    # ------------------------------------------------------------------ planner queries
+    def distance(self, q, targets, pair_idx, dtype="f64") -> np.ndarray:
+        """min over the listed active pairs of the pair distance (hpp-fcl
+        computeDistance().min_distance; <= 0 when intersecting) for each
+        configuration: q [B,nq], targets [B,12] (or one row, broadcast) -> [B]."""
+        code, npt = _dtype(dtype)
+        qq = np.ascontiguousarray(q, dtype=npt).reshape(-1, self.nq)
+        tg = np.ascontiguousarray(np.broadcast_to(np.asarray(targets, dtype=npt).reshape(-1, 12), (qq.shape[0], 12)))
+        idx = np.ascontiguousarray(pair_idx, dtype=np.int32).reshape(-1)
+        out = np.empty(qq.shape[0], dtype=npt)
+        _lib.check(self.lib.ikg_distance_batch(self._h, self.device, code, qq.ctypes.data, tg.ctypes.data,
+                                               qq.shape[0], idx.ctypes.data, idx.size, out.ctypes.data, None,
+                                               _lib.IKG_FLAG_HOST_POINTERS))
+        return out
+
+    def pair_distances(self, q, targets, pair_idx, dtype="f64") -> np.ndarray:
+        """Each listed pair's distance: [B, len(pair_idx)] (one query per pair)."""
+        return np.stack([self.distance(q, targets, [k], dtype) for k in pair_idx], axis=1)
+
+    def target_env(self, targets, geoms, dtype="f64") -> np.ndarray:
+        """The scene's target geometry at each placement [B,12] against the
+        listed world-fixed geometries -> bool [B] (path.py:51-52)."""
+        code, npt = _dtype(dtype)
+        tg = np.ascontiguousarray(targets, dtype=npt).reshape(-1, 12)
+        g = np.ascontiguousarray(geoms, dtype=np.int32).reshape(-1)
+        out = np.empty(tg.shape[0], dtype=np.uint8)
+        _lib.check(self.lib.ikg_target_env_batch(self._h, self.device, code, tg.ctypes.data, tg.shape[0],
+                                                 g.ctypes.data, g.size, out.ctypes.data, None,
+                                                 _lib.IKG_FLAG_HOST_POINTERS))
+        return out.astype(bool)
+
     # ------------------------------------------------------------------ log6
     def log6(self, M, dtype="f64") -> np.ndarray:
         """pin.log6 of placements [B,12] -> [B,6] ([v; w])."""

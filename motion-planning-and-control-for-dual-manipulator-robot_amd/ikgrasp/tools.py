@@ -2,8 +2,8 @@
 
 Same names and argument meaning.  `collision` runs the HIP collision kernel
 (ikg_collision_batch) on the robot's scene with the cube at its current
-placement; `distanceToObstacle` is out of the current scope and
-raises NotImplementedError rather than silently answering.
+placement; `distanceToObstacle` runs the HIP distance kernel
+(ikg_distance_batch) over the same pairs as the reference.
 """
 from __future__ import annotations
 
@@ -59,5 +59,23 @@ def collision(robot, q):
     return bool(solver.collision(np.asarray(q, dtype=np.float64).reshape(1, -1), target)[0])
 
 
+def _scene_of(robot):
+    solver = robot.solver
+    if solver.scene is None:
+        raise RuntimeError("robot has no collision scene attached (ikgrasp.scene.setuppinocchio builds it)")
+    return solver, solver.scene
+
+
+def _cube_target(robot):
+    placement = robot.cube_placement if robot.cube_placement is not None else robot.cube_default
+    R, t = as_rt(placement)
+    return np.concatenate([R.reshape(9), t])[None, :]
+
+
 def distanceToObstacle(robot, q):
-    raise NotImplementedError("distance queries are out of the current scope (SURVEY §8f-2)")
+    """tools.py:37-51 — shortest distance between the robot and the obstacle /
+    table: min over the active pairs whose second geometry is
+    'obstaclebase_0' or 'baseLink_0' of hpp-fcl's min_distance (GPU GJK)."""
+    solver, scene = _scene_of(robot)
+    d = solver.distance(np.asarray(q, dtype=np.float64).reshape(1, -1), _cube_target(robot), scene.obstacle_pairs())
+    return float(d[0])

@@ -19,6 +19,13 @@
    geometry inflated and deflated by 1e-9 m / 1e-4 m).
 5. `collision_solve_cases.npz` — computeqgrasppose WITH the collision term
    (collision_oracle.computeqgrasppose) on the oracle_cases inputs.
+6. `planner_cases.npz` — the planner row answered by
+   oracle/planner_oracle.py: per-pair distances of the distanceToObstacle pairs
+   at the oracle solutions and at random configurations; cube-vs-environment
+   checks of random placements (with 1e-9 m robustness flags);
+   sample_cube_placement for np.random seeds 0..2 (placement, q, attempts and
+   the next draw of the stream); project_path between samples 0 and 1 and from
+   the KAT-1 solution towards sample 0.
 """
 import json
 import os
@@ -174,8 +181,71 @@ def make_collision_solve_cases():
           "(convergence-only:", int(c["converged"].sum()), ")")
 
 
+def _pair_dists(args):
+    from oracle import planner_oracle
+    q, target = args
+    import warnings
+    warnings.filterwarnings("ignore")
+    sc = _scene()
+    return planner_oracle.pair_distances(sc, q, target[:9].reshape(3, 3), target[9:], planner_oracle.obstacle_pairs(sc))
+
+
+def _env_query(t):
+    from oracle import planner_oracle
+    res = []
+    for delta in (0.0, 1e-9, -1e-9):
+        sc = _scaled(_scene(), delta)
+        res.append(planner_oracle.target_env(sc, t[:9].reshape(3, 3), t[9:]))
+    return res[0], res[0] == res[1] == res[2]
+
+
+def make_planner_cases(n_random=32, n_env=256):
+    import warnings
+    warnings.filterwarnings("ignore")
+    from oracle import planner_oracle
+    sc = _scene()
+    model = load_nextage()
+    c = np.load(os.path.join(HERE, "oracle_cases.npz"))
+    kat = json.load(open(os.path.join(HERE, "kat.json")))
+    q_rand = random_seeds(model, n_random, seed=21)
+    qs = np.concatenate([c["q"], q_rand])
+    tg = np.concatenate([c["targets"], np.repeat(c["targets"][:1], n_random, 0)])
+    with Pool(8) as p:
+        dists = np.array(p.map(_pair_dists, list(zip(qs, tg))))
+    rng = np.random.default_rng(22)
+    env_t = np.zeros((n_env, 12))
+    env_t[:, [0, 4, 8]] = 1.0
+    env_t[:, 9] = rng.uniform(0.25, 0.55, n_env)
+    env_t[:, 10] = rng.uniform(-0.35, 0.15, n_env)
+    env_t[:, 11] = rng.uniform(0.85, 1.15, n_env)
+    with Pool(8) as p:
+        env = np.array(p.map(_env_query, list(env_t)))
+    start_t, goal_t = np.array(kat["cube_placement"]["t"]), np.array(kat["cube_placement_target"]["t"])
+    samples = []
+    for seed in range(3):
+        rs = np.random.RandomState(seed)
+        q, t, att = planner_oracle.sample_cube_placement(sc, rs, start_t, goal_t)
+        samples.append((q, t, att, rs.random_sample()))
+    I = np.eye(3)
+    # A: sample 0 -> sample 1 (completes); B: KAT-1 solution -> sample 0 (the
+    # warm-started solve of the first step fails: the valid prefix is the start)
+    rpath, cpath = planner_oracle.project_path(sc, samples[0][0], (I, samples[0][1]), (I, samples[1][1]))
+    rpath_b, cpath_b = planner_oracle.project_path(sc, np.array(kat["q0"]), (I, start_t), (I, samples[0][1]))
+    np.savez_compressed(
+        os.path.join(HERE, "planner_cases.npz"), pair_idx=np.array(planner_oracle.obstacle_pairs(sc), dtype=np.int32),
+        dist_q=qs, dist_targets=tg, dist=dists, env_targets=env_t, env_hit=env[:, 0], env_robust=env[:, 1],
+        sample_q=np.array([s[0] for s in samples]), sample_t=np.array([s[1] for s in samples]),
+        sample_attempts=np.array([s[2] for s in samples]), sample_next=np.array([s[3] for s in samples]),
+        path_start_q=samples[0][0], path_start_t=samples[0][1], path_goal_t=samples[1][1],
+        path_q=np.array(rpath), path_t=np.array([p[1] for p in cpath]),
+        pathb_start_q=np.array(kat["q0"]), pathb_start_t=start_t, pathb_goal_t=samples[0][1],
+        pathb_q=np.array(rpath_b), pathb_t=np.array([p[1] for p in cpath_b]))
+    print("wrote planner_cases.npz:", dists.shape, "distances,", int(env[:, 0].sum()), "/", n_env,
+          "colliding placements,", "samples", [(s[2]) for s in samples], "path lengths", len(rpath), len(rpath_b))
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kat", "cases", "scene", "collision", "collision_solve"]
+    what = sys.argv[1:] or ["kat", "cases", "scene", "collision", "collision_solve", "planner"]
     if os.path.isdir(REF) and "kat" in what:
         make_kats()
     if "cases" in what:
@@ -186,3 +256,5 @@ if __name__ == "__main__":
         make_collision_cases()
     if "collision_solve" in what:
         make_collision_solve_cases()
+    if "planner" in what:
+        make_planner_cases()

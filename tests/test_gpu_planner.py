@@ -1,0 +1,121 @@
+"""Planner row on the GPU against the planner oracle's golden
+fixtures (tests/golden/planner_cases.npz, oracle/planner_oracle.py):
+
+  * pair distances of the distanceToObstacle pairs (GPU GJK vs the oracle's
+    GJK-free exact / least-squares / convex-program distances): separated
+    pairs within 1e-7 m, intersecting pairs <= 1e-9;
+  * tools.distanceToObstacle = the minimum over those pairs;
+  * the cube-vs-environment check: identical on every robust placement;
+  * path.sample_cube_placement with np.random seeded as the reference would
+    be: the same placement (bit-exact draws), q within 1e-9 (fp64 IK parity
+    bar), the same next draw of the stream;
+  * path.project_path: the same valid prefix, q within 1e-9; project_paths
+    (many chains per launch) equals the per-chain drop-in.
+Distance parity against hpp-fcl itself is unpinned (hpp-fcl is absent).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pc():
+    return dict(np.load(os.path.join(GOLDEN, "planner_cases.npz")))
+
+
+@pytest.fixture(scope="module")
+def robot_cube():
+    import ikgrasp
+    robot, _, _, cube = ikgrasp.setuppinocchio()
+    return robot, cube
+
+
+def test_pair_distances_match_oracle(robot_cube, pc):
+    robot, _ = robot_cube
+    s = robot.solver
+    d = s.pair_distances(pc["dist_q"], pc["dist_targets"], pc["pair_idx"])
+    ref = pc["dist"]
+    sep = ref > 1e-6
+    assert sep.mean() > 0.5
+    assert np.abs(d[sep] - ref[sep]).max() <= 1e-7
+    assert (d[ref <= 0.0] <= 1e-9).all()
+
+
+def test_min_distance_and_dropin(robot_cube, pc):
+    from ikgrasp.tools import distanceToObstacle
+    robot, _ = robot_cube
+    s = robot.solver
+    dmin = s.distance(pc["dist_q"], pc["dist_targets"], pc["pair_idx"])
+    ref = pc["dist"].min(axis=1)
+    ok = ref > 1e-6
+    assert np.abs(dmin[ok] - ref[ok]).max() <= 1e-7
+    for i in np.nonzero(ok)[0][:4]:
+        assert abs(distanceToObstacle(robot, pc["dist_q"][i]) - ref[i]) <= 1e-7
+    # fp32 query path
+    d32 = s.distance(pc["dist_q"], pc["dist_targets"], pc["pair_idx"], dtype="f32")
+    assert np.abs(d32[ok] - ref[ok]).max() <= 1e-4
+
+
+def test_cube_environment_check(robot_cube, pc):
+    robot, _ = robot_cube
+    s = robot.solver
+    hit = s.target_env(pc["env_targets"], s.scene.env_geoms())
+    rob = pc["env_robust"].astype(bool)
+    assert rob.mean() > 0.95
+    assert np.array_equal(hit[rob], pc["env_hit"].astype(bool)[rob])
+    assert 0 < hit.sum() < len(hit)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_sample_cube_placement_dropin(robot_cube, pc, seed):
+    from ikgrasp.config import CUBE_PLACEMENT, CUBE_PLACEMENT_TARGET
+    from ikgrasp.path import sample_cube_placement
+    robot, cube = robot_cube
+    np.random.seed(seed)
+    q, placement = sample_cube_placement(robot, cube, CUBE_PLACEMENT, CUBE_PLACEMENT_TARGET, batch=8)
+    assert np.array_equal(placement.translation, pc["sample_t"][seed])
+    assert np.array_equal(placement.rotation, np.eye(3))
+    assert np.abs(q - pc["sample_q"][seed]).max() <= 1e-9
+    assert np.random.random_sample() == pc["sample_next"][seed]
+    assert np.array_equal(cube.placement.translation, placement.translation)  # setcubeplacement side effect
+
+
+def test_project_path_dropin(robot_cube, pc):
+    from ikgrasp.path import project_path
+    from ikgrasp.se3 import SE3
+    robot, cube = robot_cube
+    for key in ("path", "pathb"):
+        rp, cp = project_path(robot, cube, pc[f"{key}_start_q"], SE3(np.eye(3), pc[f"{key}_start_t"]),
+                              SE3(np.eye(3), pc[f"{key}_goal_t"]))
+        assert len(rp) == len(pc[f"{key}_q"]) and len(cp) == len(rp)
+        assert np.abs(np.array(rp) - pc[f"{key}_q"]).max() <= 1e-9
+        assert np.abs(np.array([p.translation for p in cp]) - pc[f"{key}_t"]).max() <= 1e-15
+
+
+def test_project_paths_batch_equals_dropin(robot_cube, pc):
+    from ikgrasp.path import project_path, project_paths
+    from ikgrasp.se3 import SE3
+    robot, cube = robot_cube
+    keys = ["path", "pathb", "path"]
+    batch = project_paths(robot, [pc[f"{k}_start_q"] for k in keys], [SE3(np.eye(3), pc[f"{k}_start_t"]) for k in keys],
+                          [SE3(np.eye(3), pc[f"{k}_goal_t"]) for k in keys])
+    for k, (rp, cp) in zip(keys, batch):
+        one, _ = project_path(robot, cube, pc[f"{k}_start_q"], SE3(np.eye(3), pc[f"{k}_start_t"]),
+                              SE3(np.eye(3), pc[f"{k}_goal_t"]))
+        assert len(rp) == len(one)
+        assert np.array_equal(np.array(rp), np.array(one))
+
+
+def test_planner_queries_reject_bad_arguments(robot_cube):
+    from ikgrasp._lib import IkgError
+    robot, _ = robot_cube
+    s = robot.solver
+    with pytest.raises(IkgError):
+        s.distance(np.zeros((1, 15)), np.zeros(12), [100000])
+    with pytest.raises(IkgError):
+        s.target_env(np.zeros((1, 12)), [s.scene.geom_id("cubebase_0")])
