@@ -166,6 +166,13 @@ def main():
         stats = torch.cat([t_max, counts])
     elapsed, kern_ms, tot_conv, tot_B, tot_iters = stats.tolist()
 
+    # the batch kernel the C-ABI dispatches (ikg_kernels.hip launch_pair_batch): the packed fp32
+    # layout from B >= 65,536 on 256 CUs (2 pair waves per SIMD), else the pair layout
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    packed = args.dtype == "f32" and (args.variant == _lib.IKG_VARIANT_PACKED or
+                                      (args.variant == _lib.IKG_VARIANT_AUTO and B * max(S, 1) >= cus * 4 * 2 * 32))
+    kname = "ikg_packed_batch_kernel" if packed else "ikg_pair_batch_kernel"
+    layout = "packed layout (both arms per lane, 64 problems/wave)" if packed else "pair layout (2 lanes/problem)"
     if rank == 0:
         per_step = elapsed / args.steps
         value = tot_conv / per_step
@@ -187,7 +194,7 @@ def main():
                 "workload": (f"BASELINE configs[4]: multi-start {S} seeds x {B} targets per GPU, {args.dtype}"
                              if S else
                              f"BASELINE configs[1]: batch {B} grasp targets per GPU, {args.dtype}, "
-                             f"pair kernel (2 lanes/problem)") +
+                             f"{layout}") +
                             (" + collision term (continuation kernel)" if args.collision else ""),
                 "collision_term": bool(args.collision),
                 "seeds_per_target": S or 1,
@@ -200,7 +207,7 @@ def main():
             "roofline": {
                 "bound": "valu", "achieved": flops, "peak": PEAK_VALU[args.dtype], "unit": "TFLOP/s",
                 "frac": flops / PEAK_VALU[args.dtype] if flops else None, "traffic": traffic,
-                "kernel": "ikg_pair_batch_kernel" + (" + ikg_collide_continue_kernel" if args.collision else ""),
+                "kernel": kname + (" + ikg_collide_continue_kernel" if args.collision else ""),
                 "kernel_ms": kern_ms,
                 "work": f"sum(iters)={sum_iters} x {F_ITER} FP ops (SURVEY §8a)",
             },

@@ -16,7 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def per_dispatch(d, counter):
     vals = {}
     for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
-        if "ikg_pair_batch_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter:
+        if ("ikg_pair_batch_kernel" in r["Kernel_Name"] or "ikg_packed_batch_kernel" in r["Kernel_Name"]) \
+                and r["Counter_Name"] == counter:
             vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return list(vals.values())
 
@@ -25,7 +26,8 @@ def main(pmc_dir, dtype, B, tag):
     fetch = statistics.median(per_dispatch(os.path.join(pmc_dir, f"fetch_b{B}_{dtype}"), "FETCH_SIZE"))
     write = statistics.median(per_dispatch(os.path.join(pmc_dir, f"write_b{B}_{dtype}"), "WRITE_SIZE"))
     out = {
-        "kernel": "ikg_pair_batch_kernel", "dtype": dtype, "batch": B, "round": tag,
+        "kernel": "ikg_packed_batch_kernel" if (dtype == "f32" and B >= 65536) else "ikg_pair_batch_kernel",
+        "dtype": dtype, "batch": B, "round": tag,
         "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write,
         "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
         "note": "2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes; median over dispatches",
