@@ -199,6 +199,41 @@ int ikg_target_env_batch(const ikg_model* model, int device, int dtype, const vo
                          const int32_t* geoms, int32_t n_geoms, uint8_t* in_collision, void* stream,
                          uint32_t flags);
 
+/*
+ * Controller kinematics: the kinematic terms of the
+ * task-space controller, control.py:284-345, for a batch of states.
+ * Replaces, per state and per hand (LARM_EFF, RARM_EFF):
+ *   pin.computeAllTerms + updateFramePlacements -> data.oMf     (control.py:284-287, :305)
+ *   pin.getFrameVelocity(model, data, fid, rf)                  (:310-313)
+ *   pin.computeFrameJacobian(model, data, q, fid, rf)           (:341-342)
+ *   pin.getFrameJacobianTimeVariation(model, data, fid, rf)     (:343-344)
+ *   J_dot @ vq                                                  (:345)
+ *   the desired-state FK (:292-294) and the PD errors (:314-333)
+ * rf: enum ikg_reference_frame (the controller uses LOCAL_WORLD_ALIGNED).
+ *   q, v [B,nq] (v may be NULL = zero velocity); q_des, v_des [B,nq] are only
+ *   read for err/derr (v_des NULL = 0).  Every output is optional (NULL):
+ *   placement [B,2,12]   oMf of LARM_EFF, RARM_EFF
+ *   velocity  [B,2,6]    frame velocity in rf
+ *   J, dJ     [B,12,nq]  rows 0-5 LARM_EFF, 6-11 RARM_EFF (np.vstack, :369), in rf;
+ *                        dJ = d/dt J along q' = v
+ *   dJv       [B,12]     dJ v
+ *   err       [B,12]     per hand [x_des - x; log3(R_des R^T)]     (:326-327)
+ *   derr      [B,12]     per hand v_des - v, LOCAL_WORLD_ALIGNED   (:330-331)
+ */
+enum ikg_reference_frame { IKG_WORLD = 0, IKG_LOCAL = 1, IKG_LOCAL_WORLD_ALIGNED = 2 };
+typedef struct ikg_frame_kin_out {
+  void* placement;
+  void* velocity;
+  void* J;
+  void* dJ;
+  void* dJv;
+  void* err;
+  void* derr;
+} ikg_frame_kin_out;
+int ikg_frame_kinematics_batch(const ikg_model* model, int device, int dtype, const void* q, const void* v,
+                               const void* q_des, const void* v_des, int64_t B, int rf,
+                               const ikg_frame_kin_out* out, void* stream, uint32_t flags);
+
 /* Thread-local message of the last failure ("" if none). */
 const char* ikg_last_error(void);
 

@@ -705,3 +705,66 @@ int ikg_target_env_batch(const ikg_model* model, int device, int dtype, const vo
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ controller kinematics
+template <typename T>
+int frame_kin_t(ikg_model* model, int device, const void* q, const void* v, const void* qd, const void* vd, int64_t B,
+                int rf, const ikg_frame_kin_out& out, hipStream_t s, uint32_t flags) {
+  const ikg::KModel<T>* dm = nullptr;
+  int rc = model->device_tables<T>(device, &dm);
+  if (rc) return rc;
+  const int nq = model->desc.nq;
+  const size_t sz[7] = {24, 12, (size_t)12 * nq, (size_t)12 * nq, 12, 12, 12};  // per state
+  void* host_out[7] = {out.placement, out.velocity, out.J, out.dJ, out.dJv, out.err, out.derr};
+  void* dev_out[7];
+  Staging st(s);
+  const bool host = flags & IKG_FLAG_HOST_POINTERS;
+  const void *dq = q, *dv = v, *dqd = qd, *dvd = vd;
+  const bool des = out.err || out.derr;
+  if (host) {
+    dq = st.in(q, sizeof(T) * nq * B);
+    dv = st.in(v, sizeof(T) * nq * B);
+    if (des) {
+      dqd = st.in(qd, sizeof(T) * nq * B);
+      dvd = st.in(vd, sizeof(T) * nq * B);
+    }
+  }
+  for (int i = 0; i < 7; ++i) dev_out[i] = host && host_out[i] ? st.out(sizeof(T) * sz[i] * B) : host_out[i];
+  if (st.rc) return st.rc;
+  ikg::FrameKinOut o{dev_out[0], dev_out[1], dev_out[2], dev_out[3], dev_out[4], dev_out[5], dev_out[6]};
+  hipError_t e = ikg::launch_frame_kin<T>(dm, nq, dq, dv, des ? dqd : nullptr, des ? dvd : nullptr, B, rf, o, s);
+  if (e != hipSuccess) return hip_fail(e, "ikg frame kinematics kernel launch");
+  if (host) {
+    for (int i = 0; i < 7; ++i)
+      if (host_out[i]) st.back(host_out[i], dev_out[i], sizeof(T) * sz[i] * B);
+    if (st.rc) return st.rc;
+    e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
+  }
+  return IKG_OK;
+}
+
+extern "C" {
+
+int ikg_frame_kinematics_batch(const ikg_model* model, int device, int dtype, const void* q, const void* v,
+                               const void* q_des, const void* v_des, int64_t B, int rf,
+                               const ikg_frame_kin_out* out, void* stream, uint32_t flags) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (!out) return fail(IKG_EINVAL, "out is NULL");
+  if (B < 0) return fail(IKG_EINVAL, "B must be >= 0");
+  if (rf < IKG_WORLD || rf > IKG_LOCAL_WORLD_ALIGNED) return fail(IKG_EINVAL, "rf %d unknown", rf);
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  if (B > 0 && !q) return fail(IKG_EINVAL, "q is required");
+  if (B > 0 && (out->err || out->derr) && !q_des) return fail(IKG_EINVAL, "err/derr need q_des");
+  if (B > (int64_t)1 << 40) return fail(IKG_EINVAL, "B too large");
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  if (B == 0) return IKG_OK;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == IKG_F64 ? frame_kin_t<double>(m, device, q, v, q_des, v_des, B, rf, *out, s, flags)
+                          : frame_kin_t<float>(m, device, q, v, q_des, v_des, B, rf, *out, s, flags);
+}
+
+}  // extern "C"

@@ -87,4 +87,18 @@ template <typename T>
 hipError_t launch_target_env(const KCollision<T>* dc, const void* targets, int64_t B, const int32_t* geoms,
                              int n_geoms, uint8_t* out, hipStream_t s);
 
+// controller kinematics (ikg_control.hip): optional outputs
+struct FrameKinOut {
+  void* placement;  // [B,2,12]
+  void* velocity;   // [B,2,6]
+  void* J;          // [B,12,nq]
+  void* dJ;         // [B,12,nq]
+  void* dJv;        // [B,12]
+  void* err;        // [B,12]
+  void* derr;       // [B,12]
+};
+template <typename T>
+hipError_t launch_frame_kin(const KModel<T>* dm, int nq, const void* q, const void* v, const void* qd, const void* vd,
+                            int64_t B, int rf, const FrameKinOut& o, hipStream_t s);
+
 }  // namespace ikg

@@ -245,3 +245,51 @@ class IKSolver:
         _lib.check(self.lib.ikg_fk_batch(self._h, self.device, code, qq.ctypes.data, qq.shape[0],
                                          out.ctypes.data, None, _lib.IKG_FLAG_HOST_POINTERS))
         return out
+
+    # ------------------------------------------------------------------ controller kinematics
+    FRAME_KIN_OUTPUTS = ("placement", "velocity", "J", "dJ", "dJv", "err", "derr")
+
+    def frame_kinematics(self, q, v=None, q_des=None, v_des=None, rf=_lib.IKG_LOCAL_WORLD_ALIGNED,
+                         outputs=("placement", "velocity", "J", "dJ", "dJv"), dtype="f64", stream=None) -> dict:
+        """ikg_frame_kinematics_batch: per state and hand (LARM_EFF, RARM_EFF)
+        the kinematic terms of control.py:284-345 in reference frame `rf`.
+        q, v [B,nq] (numpy, or torch tensors on a ROCm device); q_des / v_des
+        only for 'err' / 'derr'.  Returns {name: array} with placement [B,2,12],
+        velocity [B,2,6], J / dJ [B,12,nq], dJv / err / derr [B,12]."""
+        unknown = set(outputs) - set(self.FRAME_KIN_OUTPUTS)
+        if unknown:
+            raise ValueError(f"unknown outputs {sorted(unknown)}")
+        nq = self.nq
+        shapes = {"placement": (2, 12), "velocity": (2, 6), "J": (12, nq), "dJ": (12, nq), "dJv": (12,),
+                  "err": (12,), "derr": (12,)}
+        if ("err" in outputs or "derr" in outputs) and q_des is None:
+            raise ValueError("err/derr need q_des")
+        if _is_torch(q):
+            import torch
+            code, _ = _dtype(q.dtype)
+            dev = q.device
+            prep = lambda x: None if x is None else x.to(device=dev, dtype=q.dtype).contiguous().view(-1, nq)
+            qq, vv, qd, vd = prep(q), prep(v), prep(q_des), prep(v_des)
+            B = qq.shape[0]
+            res = {k: torch.empty((B,) + shapes[k], dtype=q.dtype, device=dev) for k in outputs}
+            ptr = lambda x: None if x is None else x.data_ptr()
+            out = _lib.FrameKinOut(*[ptr(res.get(k)) for k in self.FRAME_KIN_OUTPUTS])
+            s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+            _lib.check(self.lib.ikg_frame_kinematics_batch(
+                self._h, dev.index or 0, code, ptr(qq), ptr(vv), ptr(qd), ptr(vd), B, int(rf), C.byref(out),
+                C.c_void_p(s), 0))
+            return res
+        code, npt = _dtype(dtype)
+        prep = lambda x: None if x is None else np.ascontiguousarray(x, dtype=npt).reshape(-1, nq)
+        qq, vv, qd, vd = prep(q), prep(v), prep(q_des), prep(v_des)
+        B = qq.shape[0]
+        for name, x in (("v", vv), ("q_des", qd), ("v_des", vd)):
+            if x is not None and x.shape[0] != B:
+                raise ValueError(f"{name} has {x.shape[0]} rows, q has {B}")
+        res = {k: np.empty((B,) + shapes[k], dtype=npt) for k in outputs}
+        ptr = lambda x: None if x is None else x.ctypes.data
+        out = _lib.FrameKinOut(*[ptr(res.get(k)) for k in self.FRAME_KIN_OUTPUTS])
+        _lib.check(self.lib.ikg_frame_kinematics_batch(
+            self._h, self.device, code, ptr(qq), ptr(vv), ptr(qd), ptr(vd), B, int(rf), C.byref(out), None,
+            _lib.IKG_FLAG_HOST_POINTERS))
+        return res

@@ -26,6 +26,13 @@
    sample_cube_placement for np.random seeds 0..2 (placement, q, attempts and
    the next draw of the stream); project_path between samples 0 and 1 and from
    the KAT-1 solution towards sample 0.
+7. `control_cases.npz` — the controller row answered by
+   oracle/control_oracle.py: desired states (q_des, vq_des) are the reference's
+   own trajectories (trajectory.json / trajectory2.json Bezier control points,
+   evaluated with control.py:38-46's Horner scheme at 24 times each), actual
+   states are those plus a seeded tracking error, plus 32 random states within
+   the joint limits; outputs are the frame placements, velocities, J, dJ, dJ v
+   in WORLD / LOCAL / LOCAL_WORLD_ALIGNED and the PD errors e, e_dot.
 """
 import json
 import os
@@ -244,8 +251,55 @@ def make_planner_cases(n_random=32, n_env=256):
           "colliding placements,", "samples", [(s[2]) for s in samples], "path lengths", len(rpath), len(rpath_b))
 
 
+def _bezier(points, t, t_min, t_max, mult_t):
+    """control.py:38-46 Bezier.eval_horner (data generation only)."""
+    pts = [np.asarray(p, dtype=np.float64) for p in points]
+    deg = len(pts) - 1
+    u = (t - t_min) / (t_max - t_min)
+    u_op, bc, tn = 1.0 - u, 1, 1
+    tmp = pts[0] * u_op
+    for i in range(1, deg):
+        tn *= u
+        bc *= (deg - i + 1) / i
+        tmp = (tmp + tn * bc * pts[i]) * u_op
+    return (tmp + tn * u * pts[-1]) * mult_t
+
+
+def make_control_cases(n_times=24, n_random=32):
+    from oracle import control_oracle
+    from oracle import ik_oracle as ik
+    rng = np.random.default_rng(31)
+    qd, vd = [], []
+    for name in ("trajectory.json", "trajectory2.json"):
+        tr = json.load(open(os.path.join(REF, name)))
+        t0, t1, m = tr["t_min"], tr["t_max"], tr["mult_t"]
+        for t in np.linspace(t0, t1, n_times):
+            qd.append(_bezier(tr["q_control_points"], t, t0, t1, m))
+            # vq_of_t as load_trajectory_from_json builds it (control.py:229-237)
+            vd.append(_bezier(tr["vq_control_points"], t, t0, t1, m))
+    qd, vd = np.array(qd), np.array(vd)
+    q = qd + rng.normal(scale=0.02, size=qd.shape)
+    v = vd + rng.normal(scale=0.05, size=vd.shape)
+    q_r = rng.uniform(ik.LOWER, ik.UPPER, size=(n_random, ik.NQ))
+    v_r = rng.normal(scale=1.0, size=(n_random, ik.NQ))
+    qd_r = q_r + rng.normal(scale=0.1, size=q_r.shape)
+    vd_r = v_r + rng.normal(scale=0.3, size=v_r.shape)
+    q, v = np.concatenate([q, q_r]), np.concatenate([v, v_r])
+    qd, vd = np.concatenate([qd, qd_r]), np.concatenate([vd, vd_r])
+    out = {"q": q, "v": v, "q_des": qd, "v_des": vd}
+    for rf in (0, 1, 2):
+        rs = [control_oracle.frame_kinematics(q[i], v[i], rf, qd[i], vd[i]) for i in range(len(q))]
+        for k in ("placement", "velocity", "J", "dJ", "dJv"):
+            out[f"{k}_rf{rf}"] = np.array([r[k] for r in rs])
+        if rf == 2:
+            out["err"] = np.array([r["err"] for r in rs])
+            out["derr"] = np.array([r["derr"] for r in rs])
+    np.savez_compressed(os.path.join(HERE, "control_cases.npz"), **out)
+    print("wrote control_cases.npz:", len(q), "states")
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kat", "cases", "scene", "collision", "collision_solve", "planner"]
+    what = sys.argv[1:] or ["kat", "cases", "scene", "collision", "collision_solve", "planner", "control"]
     if os.path.isdir(REF) and "kat" in what:
         make_kats()
     if "cases" in what:
@@ -258,3 +312,5 @@ if __name__ == "__main__":
         make_collision_solve_cases()
     if "planner" in what:
         make_planner_cases()
+    if os.path.isdir(REF) and "control" in what:
+        make_control_cases()
