@@ -732,7 +732,7 @@ int frame_kin_t(ikg_model* model, int device, const void* q, const void* v, cons
   for (int i = 0; i < 7; ++i) dev_out[i] = host && host_out[i] ? st.out(sizeof(T) * sz[i] * B) : host_out[i];
   if (st.rc) return st.rc;
   ikg::FrameKinOut o{dev_out[0], dev_out[1], dev_out[2], dev_out[3], dev_out[4], dev_out[5], dev_out[6]};
-  hipError_t e = ikg::launch_frame_kin<T>(dm, nq, dq, dv, des ? dqd : nullptr, des ? dvd : nullptr, B, rf, o, s);
+  hipError_t e = ikg::launch_frame_kin<T>(dm, nq, model->spec, dq, dv, des ? dqd : nullptr, des ? dvd : nullptr, B, rf, o, s);
   if (e != hipSuccess) return hip_fail(e, "ikg frame kinematics kernel launch");
   if (host) {
     for (int i = 0; i < 7; ++i)

@@ -22,9 +22,10 @@
 //   dJ col k (LWA) = [a'_k x (p_f - o_k) + a_k x (p'_f - o'_k); a'_k],   a'_k = w_{k-1} x a_k
 // (a_k world axis, o_k world origin, o'_k its velocity, w_{k-1} the angular
 // velocity of the parent body).  The dense [12, nq] matrices of the tile's 32
-// states are assembled in LDS (zeros written once per workgroup; every tile
-// writes the same non-zero positions) and streamed out with 16-byte coalesced
-// stores: the kernel is bound by those writes.
+// states are assembled in LDS (zeroed once; every matrix writes the same
+// non-zero positions) and streamed out with 16-byte coalesced stores.  Storing
+// the rows straight from the lanes (8-byte stores 120 B apart across lanes)
+// was measured 3.5x slower.
 #include <hip/hip_runtime.h>
 
 #include "ikg_launch.hpp"
@@ -33,7 +34,10 @@ namespace ikg {
 
 namespace {
 
-constexpr int kStatesPerTile = 32;
+#ifndef IKG_FK_TILE
+#define IKG_FK_TILE 32
+#endif
+constexpr int kStatesPerTile = IKG_FK_TILE;
 
 template <typename T>
 __device__ inline void cross3(const T* a, const T* b, T* c) {
@@ -42,57 +46,148 @@ __device__ inline void cross3(const T* a, const T* b, T* c) {
   c[2] = a[0] * b[1] - a[1] * b[0];
 }
 
-// One joint of the hand's support chain: parent body frame (R, o), the point
-// velocity o' of the current origin and the parent body's angular velocity w
-// advance across joint j (placement (jR, jt), axis, angle (s, c), rate vj).
-// Out: the joint's world axis a, its derivative a' = w_parent x a.
+// sin/cos of a joint angle: Cody-Waite reduction by pi/2 in three FMA parts
+// and Taylor polynomials on |r| <= pi/4 (truncation < 1e-17; ~1 ulp overall).
+// The reduction stays within ~1e-16 absolute for |x| < 2^40 (fp64; fp32:
+// |x| < 2^16), far beyond any joint angle.  It replaces OCML's sincos, whose
+// Payne-Hanek path for huge arguments dominated the code of the first version.
+template <typename T>
+__device__ inline void joint_sincos(T x, T* s, T* c) {
+  const T n = rint(x * T(0.63661977236758134308));  // 2/pi
+  T r;
+  if constexpr (sizeof(T) == 8) {
+    r = fma(-n, 1.5707963267948966, x);
+    r = fma(-n, 6.123233995736766e-17, r);
+    r = fma(-n, -1.4973849048591698e-33, r);
+  } else {
+    r = fmaf(-n, 1.57079637f, x);
+    r = fmaf(-n, -4.37113883e-08f, r);
+    r = fmaf(-n, -1.71512489e-15f, r);
+  }
+  const T r2 = r * r;
+  T sp, cp;
+  if constexpr (sizeof(T) == 8) {  // sin: r (1 - r^2/3! + ... - r^14/15!), cos: 1 - r^2/2! + ... + r^16/16!
+    sp = T(-1.0 / 1307674368000.0);
+    sp = fma(sp, r2, T(1.0 / 6227020800.0));
+    sp = fma(sp, r2, T(-1.0 / 39916800.0));
+    sp = fma(sp, r2, T(1.0 / 362880.0));
+    sp = fma(sp, r2, T(-1.0 / 5040.0));
+    sp = fma(sp, r2, T(1.0 / 120.0));
+    sp = fma(sp, r2, T(-1.0 / 6.0));
+    cp = T(1.0 / 20922789888000.0);
+    cp = fma(cp, r2, T(-1.0 / 87178291200.0));
+    cp = fma(cp, r2, T(1.0 / 479001600.0));
+    cp = fma(cp, r2, T(-1.0 / 3628800.0));
+    cp = fma(cp, r2, T(1.0 / 40320.0));
+    cp = fma(cp, r2, T(-1.0 / 720.0));
+    cp = fma(cp, r2, T(1.0 / 24.0));
+  } else {
+    sp = T(1.0 / 362880.0);
+    sp = fmaf(sp, r2, T(-1.0 / 5040.0));
+    sp = fmaf(sp, r2, T(1.0 / 120.0));
+    sp = fmaf(sp, r2, T(-1.0 / 6.0));
+    cp = T(-1.0 / 3628800.0);
+    cp = fmaf(cp, r2, T(1.0 / 40320.0));
+    cp = fmaf(cp, r2, T(-1.0 / 720.0));
+    cp = fmaf(cp, r2, T(1.0 / 24.0));
+  }
+  const T sr = fma(r * r2, sp, r);
+  const T cr = fma(r2 * r2, cp, fma(r2, T(-0.5), T(1)));
+  const int qd = (int)n & 3;
+  const T ss = (qd & 1) ? cr : sr;
+  const T cc = (qd & 1) ? sr : cr;
+  *s = (qd & 2) ? -ss : ss;
+  *c = ((qd + 1) & 2) ? -cc : cc;
+}
+
+// R <- R Rot_axis(s, c) and a = the axis column of R (unchanged by the
+// rotation).  Compile-time axis: the specialised two-column update; runtime
+// axis (SpecGeneric): the branch-free one-hot form R Rot = c R + s R[e]x +
+// (1 - c)(R e) e^T (a select chain over a runtime axis index is lowered to
+// scratch memory).
+template <int AX, typename T>
+__device__ inline void col_rot(T* R, int axis, T s, T c, T* a) {
+  if constexpr (AX != kAxRuntime) {
+    column(R, AX, a);
+    rotate_axis(R, AX, s, c);
+  } else {
+    const T e0 = T(axis == 0), e1 = T(axis == 1), e2 = T(axis == 2);
+    const T omc = T(1) - c;
+    T Rn[9];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const T r0 = R[3 * r], r1 = R[3 * r + 1], r2 = R[3 * r + 2];
+      const T u = e0 * r0 + e1 * r1 + e2 * r2;
+      a[r] = u;
+      Rn[3 * r + 0] = c * r0 + s * (e2 * r1 - e1 * r2) + omc * u * e0;
+      Rn[3 * r + 1] = c * r1 + s * (e0 * r2 - e2 * r0) + omc * u * e1;
+      Rn[3 * r + 2] = c * r2 + s * (e1 * r0 - e0 * r1) + omc * u * e2;
+    }
+#pragma unroll
+    for (int i = 0; i < 9; ++i) R[i] = Rn[i];
+  }
+}
+
+// Walk state along a hand's support chain: body frame (R, o), the velocity o'
+// of its origin and the body's angular velocity w.
 template <typename T>
 struct ChainState {
   T R[9], o[3], od[3], w[3];
 };
 
-template <typename T>
-__device__ inline void chain_joint(const KModel<T>* __restrict__ m, int j, bool first, T s, T c, T vj,
+// Advance the chain across slot k (0 = root, 1..6 = arm joint k-1) given the
+// joint's (sin, cos) and rate.  Out: the joint's world axis a and its
+// derivative a' = w_parent x a.  The placements come from the arm-structured
+// tables: model-wide addresses, so they are scalar loads and each lane selects
+// its arm's value (armc) -- no per-lane address arithmetic.  SP
+// (ikg_device.hpp Spec) gives the compile-time axis of each slot, the exact
+// zero components of the arm offsets and whether joint placements carry
+// rotations (Nextage: Z | Z,Y,Y,X,Y,Z, none); SpecGeneric reads them from the
+// model (axes are model-wide, so the runtime-axis branches stay uniform).
+template <class SP, typename T>
+__device__ inline void chain_joint(const KModel<T>* __restrict__ m, bool right, int k, T s, T c, T vj,
                                    ChainState<T>& st, T* a, T* ad) {
-  T on[3];
-  if (first) {
+  if (k == 0) {
+    const bool prot = SP::prot && ((m->rot_mask >> 6) & 1);
 #pragma unroll
-    for (int i = 0; i < 9; ++i) st.R[i] = m->jR[j][i];
+    for (int i = 0; i < 9; ++i) st.R[i] = prot ? m->root_R[i] : T(i % 4 == 0);
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      on[i] = m->jt[j][i];
+      st.o[i] = m->root_t[i];
       st.od[i] = T(0);
       st.w[i] = T(0);
     }
+    col_rot<SP::axis(0)>(st.R, m->root_axis, s, c, a);
   } else {
-    T d[3];
-    matvec3(st.R, m->jt[j], d);
-    T wd[3];
+    const int ka = k - 1;
+    T pt[3], d[3], wd[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) pt[i] = SP::zero_t(ka, i) ? T(0) : armc<T>(right, m->arm_t[0][ka][i], m->arm_t[1][ka][i]);
+    matvec3(st.R, pt, d);
     cross3(st.w, d, wd);  // velocity of the new origin: o' + w x (o_new - o)
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      on[i] = st.o[i] + d[i];
+      st.o[i] += d[i];
       st.od[i] += wd[i];
     }
-    T Rn[9];
-    matmul3(st.R, m->jR[j], Rn);
+    if constexpr (SP::prot) {
+      if (m->rot_mask & (1 << ka)) {
+        T P[9], Rn[9];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) st.R[i] = Rn[i];
-  }
+        for (int i = 0; i < 9; ++i) P[i] = armc<T>(right, m->arm_R[0][ka][i], m->arm_R[1][ka][i]);
+        matmul3(st.R, P, Rn);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) st.o[i] = on[i];
-  // Rot_axis leaves its own axis fixed; one branch per axis keeps every index
-  // compile-time (a select chain over a runtime axis is lowered to scratch)
-  const int ax = m->jaxis[j];
-  if (ax == 0) {
-    column(st.R, 0, a);
-    rotate_axis(st.R, 0, s, c);
-  } else if (ax == 1) {
-    column(st.R, 1, a);
-    rotate_axis(st.R, 1, s, c);
-  } else {
-    column(st.R, 2, a);
-    rotate_axis(st.R, 2, s, c);
+        for (int i = 0; i < 9; ++i) st.R[i] = Rn[i];
+      }
+    }
+    switch (ka) {  // k is a compile-time constant of the unrolled chain loops
+      case 0: col_rot<SP::axis(1)>(st.R, m->arm_axis[0], s, c, a); break;
+      case 1: col_rot<SP::axis(2)>(st.R, m->arm_axis[1], s, c, a); break;
+      case 2: col_rot<SP::axis(3)>(st.R, m->arm_axis[2], s, c, a); break;
+      case 3: col_rot<SP::axis(4)>(st.R, m->arm_axis[3], s, c, a); break;
+      case 4: col_rot<SP::axis(5)>(st.R, m->arm_axis[4], s, c, a); break;
+      default: col_rot<SP::axis(6)>(st.R, m->arm_axis[5], s, c, a); break;
+    }
   }
   cross3(st.w, a, ad);
 #pragma unroll
@@ -101,8 +196,8 @@ __device__ inline void chain_joint(const KModel<T>* __restrict__ m, int j, bool 
 
 // q index of chain slot k (0 = root, 1..6 = arm joints)
 template <typename T>
-__device__ inline int chain_q(const KModel<T>* __restrict__ m, int arm, int k) {
-  return k == 0 ? m->root_q : m->arm_q[arm][k - 1];
+__device__ inline int chain_q(const KModel<T>* __restrict__ m, bool right, int k) {
+  return k == 0 ? m->root_q : (right ? m->arm_q[1][k - 1] : m->arm_q[0][k - 1]);
 }
 
 template <typename T>
@@ -110,35 +205,45 @@ struct FramePass {
   T R[9], p[3], pd[3], w[3];  // effector placement, origin velocity, angular velocity (world)
 };
 
-// (sin, cos, rate) of chain slot k, read from the state's q / v rows
+// The state's chain values: (sin, cos, rate) of the root and arm joints and
+// their q indices.  All loads are issued together and the chain loops below
+// are unrolled over these registers (a rolled loop waits on one global load
+// per joint per pass: that exposed latency dominated the first version).
 template <typename T>
-__device__ inline int load_joint(const KModel<T>* __restrict__ m, int arm, int k, const T* __restrict__ qrow,
-                                 const T* __restrict__ vrow, T& s, T& c, T& vj) {
-  const int j = chain_q(m, arm, k);
-  Prec<T>::sincos_(qrow[j], &s, &c);
-  vj = vrow ? vrow[j] : T(0);
-  return j;
+struct JointVals {
+  T s[7], c[7], v[7];
+  int j[7];
+};
+
+template <typename T>
+__device__ inline void load_joints(const KModel<T>* __restrict__ m, bool right, const T* __restrict__ qrow,
+                                   const T* __restrict__ vrow, JointVals<T>& jv) {
+  T qv[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    jv.j[k] = chain_q(m, right, k);
+    qv[k] = qrow[jv.j[k]];
+    jv.v[k] = vrow ? vrow[jv.j[k]] : T(0);
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) joint_sincos(qv[k], &jv.s[k], &jv.c[k]);
 }
 
 // Forward pass to the effector frame (pin.forwardKinematics first order +
 // updateFramePlacements, frame = LARM_EFF / RARM_EFF on the last arm joint).
-// The chain loops stay rolled (the joint tables are indexed per lane), which
-// keeps the kernel far below the register file; the compute is small next to
-// the output stream.
-template <typename T>
-__device__ inline void frame_pass(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow,
-                                  const T* __restrict__ vrow, FramePass<T>& f) {
+template <class SP, typename T>
+__device__ inline void frame_pass(const KModel<T>* __restrict__ m, bool right, const JointVals<T>& jv,
+                                  FramePass<T>& f) {
   ChainState<T> st;
   T a[3], ad[3];
-#pragma unroll 1
-  for (int k = 0; k < 7; ++k) {
-    T s, c, vj;
-    const int j = load_joint(m, arm, k, qrow, vrow, s, c, vj);
-    chain_joint(m, j, k == 0, s, c, vj, st, a, ad);
-  }
-  T d[3];
-  matvec3(st.R, m->hand_t[arm], d);
-  T wd[3];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) chain_joint<SP>(m, right, k, jv.s[k], jv.c[k], jv.v[k], st, a, ad);
+  T ht[3], hR[9], d[3], wd[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ht[i] = armc<T>(right, m->hand_t[0][i], m->hand_t[1][i]);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) hR[i] = armc<T>(right, m->hand_R[0][i], m->hand_R[1][i]);
+  matvec3(st.R, ht, d);
   cross3(st.w, d, wd);
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -146,20 +251,20 @@ __device__ inline void frame_pass(const KModel<T>* __restrict__ m, int arm, cons
     f.pd[i] = st.od[i] + wd[i];
     f.w[i] = st.w[i];
   }
-  matmul3(st.R, m->hand_R[arm], f.R);
+  matmul3(st.R, hR, f.R);
 }
 
-// express a LOCAL_WORLD_ALIGNED motion column in rf (WORLD: shift to the world
+// express a LOCAL_WORLD_ALIGNED motion column in RF (WORLD: shift to the world
 // origin; LOCAL: rotate into the frame)
-template <typename T>
-__device__ inline void to_rf(int rf, const FramePass<T>& f, const T* lin, const T* ang, T* out) {
-  if (rf == 2) {
+template <int RF, typename T>
+__device__ inline void to_rf(const FramePass<T>& f, const T* lin, const T* ang, T* out) {
+  if constexpr (RF == 2) {
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       out[i] = lin[i];
       out[3 + i] = ang[i];
     }
-  } else if (rf == 0) {  // v_O = v_p + w x (0 - p) = v_p + p x w
+  } else if constexpr (RF == 0) {  // v_O = v_p + w x (0 - p) = v_p + p x w
     T pw[3];
     cross3(f.p, ang, pw);
 #pragma unroll
@@ -170,6 +275,70 @@ __device__ inline void to_rf(int rf, const FramePass<T>& f, const T* lin, const 
   } else {
     matvec3_t(f.R, lin, out);
     matvec3_t(f.R, ang, out + 3);
+  }
+}
+
+// column k of J (WHICH = 0) or dJ (WHICH = 1) in RF from the chain state at
+// joint k (axis a, its derivative ad) and the effector pass f
+template <int WHICH, int RF, typename T>
+__device__ inline void jac_column(const FramePass<T>& f, const ChainState<T>& st, const T* a, const T* ad, T* col) {
+  T r[3], lin[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) r[i] = f.p[i] - st.o[i];
+  if constexpr (WHICH == 0) {
+    cross3(a, r, lin);
+    to_rf<RF>(f, lin, a, col);
+  } else if constexpr (RF == 0) {  // d/dt [o x a; a] = [o' x a + o x a'; a']
+    T t3[3], t4[3];
+    cross3(st.od, a, t3);
+    cross3(st.o, ad, t4);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      col[i] = t3[i] + t4[i];
+      col[3 + i] = ad[i];
+    }
+  } else {
+    T rd[3], t1[3], t2[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) rd[i] = f.pd[i] - st.od[i];
+    cross3(ad, r, t1);
+    cross3(a, rd, t2);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) lin[i] = t1[i] + t2[i];
+    if constexpr (RF == 1) {  // d/dt (R^T J_lwa) = R^T (dJ_lwa - w x J_lwa)
+      T jl[3], wl[3], wa[3], l2[3], a2[3];
+      cross3(a, r, jl);
+      cross3(f.w, jl, wl);
+      cross3(f.w, a, wa);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        l2[i] = lin[i] - wl[i];
+        a2[i] = ad[i] - wa[i];
+      }
+      to_rf<RF>(f, l2, a2, col);
+    } else {
+      to_rf<RF>(f, lin, ad, col);
+    }
+  }
+}
+
+// Second pass along the chain: write the lane's 6 rows of column j = chain
+// joint k into `rows` (row stride nq) and accumulate dJ v (WHICH = 1).
+template <int WHICH, int RF, class SP, typename T>
+__device__ inline void emit_columns(const KModel<T>* __restrict__ m, bool right, const JointVals<T>& jv,
+                                    const FramePass<T>& f, T* rows, int nq, T* acc) {
+  ChainState<T> st;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    T a[3], ad[3], col[6];
+    chain_joint<SP>(m, right, k, jv.s[k], jv.c[k], jv.v[k], st, a, ad);
+    jac_column<WHICH, RF>(f, st, a, ad, col);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) rows[i * nq + jv.j[k]] = col[i];
+    if constexpr (WHICH == 1) {
+#pragma unroll
+      for (int i = 0; i < 6; ++i) acc[i] += col[i] * jv.v[k];
+    }
   }
 }
 
@@ -190,169 +359,132 @@ __device__ inline void tile_store(const T* __restrict__ tile, T* __restrict__ ds
 
 }  // namespace
 
-template <typename T>
+// One tile of 32 states per workgroup.  (A grid-stride loop over tiles let the
+// compiler hoist the model-table values out of the loop: more live registers.)
+template <typename T, int RF, class SP>
 __global__ __launch_bounds__(64) void ikg_frame_kin_kernel(const KModel<T>* __restrict__ m, const T* __restrict__ q,
                                                            const T* __restrict__ v, const T* __restrict__ qd,
-                                                           const T* __restrict__ vd, int64_t B, int rf,
-                                                           FrameKinOut o) {
+                                                           const T* __restrict__ vd, int64_t B, FrameKinOut o) {
   extern __shared__ __align__(16) unsigned char smem[];
   T* tile = reinterpret_cast<T*>(smem);
   const int nq = m->nq;
   const int per_state = 12 * nq;
-  const bool mats = o.J || o.dJ;
-  if (mats) {
-    for (int i = threadIdx.x; i < kStatesPerTile * per_state; i += 64) tile[i] = T(0);
-  }
   const int lane = threadIdx.x;
   const int arm = lane & 1;
+  const bool right = arm != 0;
+  const int64_t p0 = (int64_t)blockIdx.x * kStatesPerTile;
+  const int ns = (int)min((int64_t)kStatesPerTile, B - p0);
+  const int sl = lane >> 1;
+  const bool live = sl < ns;
+  const int64_t p = p0 + sl;
+  if (o.J || o.dJ) {
+    for (int i = lane; i < kStatesPerTile * per_state; i += 64) tile[i] = T(0);
+  }
+  JointVals<T> jv;
+  FramePass<T> f;
+  if (live) {
+    load_joints(m, right, q + p * nq, v ? v + p * nq : nullptr, jv);
+    frame_pass<SP>(m, right, jv, f);
+    if (o.placement) {
+      T* out = (T*)o.placement + p * 24 + arm * 12;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) out[i] = f.R[i];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) out[9 + i] = f.p[i];
+    }
+    if (o.velocity) {
+      T vf[6];
+      to_rf<RF>(f, f.pd, f.w, vf);
+      T* out = (T*)o.velocity + p * 12 + arm * 6;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) out[i] = vf[i];
+    }
+    if (o.err || o.derr) {  // control.py:314-333 (always LOCAL_WORLD_ALIGNED)
+      JointVals<T> jd;
+      FramePass<T> fd;
+      load_joints(m, right, qd + p * nq, vd ? vd + p * nq : nullptr, jd);
+      frame_pass<SP>(m, right, jd, fd);
+      if (o.err) {
+        T Re[9], zero[3] = {T(0), T(0), T(0)}, lg[6];
+        matmul3_nt(fd.R, f.R, Re);  // R_des R^T
+        log6(Re, zero, lg);         // rotation part = pin.log3
+        T* out = (T*)o.err + p * 12 + arm * 6;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          out[i] = fd.p[i] - f.p[i];
+          out[3 + i] = lg[3 + i];
+        }
+      }
+      if (o.derr) {
+        T* out = (T*)o.derr + p * 12 + arm * 6;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          out[i] = fd.pd[i] - f.pd[i];
+          out[3 + i] = fd.w[i] - f.w[i];
+        }
+      }
+    }
+  }
+  T* rows = tile + sl * per_state + 6 * arm * nq;
+  if (o.J) {
+    if (live) emit_columns<0, RF, SP>(m, right, jv, f, rows, nq, (T*)nullptr);
+    __syncthreads();
+    tile_store(tile, (T*)o.J + p0 * per_state, ns * per_state);
+    __syncthreads();
+  }
+  if (o.dJ || o.dJv) {
+    T acc[6] = {T(0), T(0), T(0), T(0), T(0), T(0)};
+    if (live) emit_columns<1, RF, SP>(m, right, jv, f, rows, nq, acc);
+    if (live && o.dJv) {
+      T* out = (T*)o.dJv + p * 12 + arm * 6;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) out[i] = acc[i];
+    }
+    if (o.dJ) {
+      __syncthreads();
+      tile_store(tile, (T*)o.dJ + p0 * per_state, ns * per_state);
+    }
+  }
+}
+
+template <typename T, int RF, class SP>
+static hipError_t launch_frame_kin_t(const KModel<T>* dm, int nq, const T* q, const T* v, const T* qd, const T* vd,
+                                     int64_t B, const FrameKinOut& o, hipStream_t s) {
   const int64_t ntiles = (B + kStatesPerTile - 1) / kStatesPerTile;
-  for (int64_t tix = blockIdx.x; tix < ntiles; tix += gridDim.x) {
-    const int64_t p0 = tix * kStatesPerTile;
-    const int ns = (int)min((int64_t)kStatesPerTile, B - p0);
-    const int sl = lane >> 1;
-    const bool live = sl < ns;
-    const int64_t p = p0 + sl;
-    const T* qrow = q + p * nq;
-    const T* vrow = v ? v + p * nq : nullptr;
-    FramePass<T> f;
-    if (live) {
-      frame_pass(m, arm, qrow, vrow, f);
-      if (o.placement) {
-        T* out = (T*)o.placement + p * 24 + arm * 12;
-#pragma unroll
-        for (int i = 0; i < 9; ++i) out[i] = f.R[i];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) out[9 + i] = f.p[i];
-      }
-      if (o.velocity) {
-        T vf[6];
-        to_rf(rf, f, f.pd, f.w, vf);
-        T* out = (T*)o.velocity + p * 12 + arm * 6;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) out[i] = vf[i];
-      }
-      if (o.err || o.derr) {  // control.py:314-333 (always LOCAL_WORLD_ALIGNED)
-        FramePass<T> fd;
-        frame_pass(m, arm, qd + p * nq, vd ? vd + p * nq : nullptr, fd);
-        if (o.err) {
-          T Re[9], zero[3] = {T(0), T(0), T(0)}, lg[6];
-          matmul3_nt(fd.R, f.R, Re);  // R_des R^T
-          log6(Re, zero, lg);         // rotation part = pin.log3
-          T* out = (T*)o.err + p * 12 + arm * 6;
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            out[i] = fd.p[i] - f.p[i];
-            out[3 + i] = lg[3 + i];
-          }
-        }
-        if (o.derr) {
-          T* out = (T*)o.derr + p * 12 + arm * 6;
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            out[i] = fd.pd[i] - f.pd[i];
-            out[3 + i] = fd.w[i] - f.w[i];
-          }
-        }
-      }
-    }
-    // J, then dJ (+ dJ v): second pass along the chain emits the columns
-#pragma unroll 1
-    for (int which = 0; which < 2; ++which) {
-      T* dst = which == 0 ? (T*)o.J : (T*)o.dJ;
-      const bool want_dJv = which == 1 && o.dJv;
-      if (!dst && !want_dJv) continue;
-      if (live) {
-        ChainState<T> st;
-        T acc[6] = {T(0), T(0), T(0), T(0), T(0), T(0)};
-        T* rows = tile + sl * per_state + 6 * arm * nq;
-#pragma unroll 1
-        for (int k = 0; k < 7; ++k) {
-          T sj, cj, vj, a[3], ad[3];
-          const int j = load_joint(m, arm, k, qrow, vrow, sj, cj, vj);
-          chain_joint(m, j, k == 0, sj, cj, vj, st, a, ad);
-          T r[3], lin[3], col[6];
-#pragma unroll
-          for (int i = 0; i < 3; ++i) r[i] = f.p[i] - st.o[i];
-          if (which == 0) {
-            cross3(a, r, lin);
-            to_rf(rf, f, lin, a, col);
-          } else {
-            T rd[3], t1[3], t2[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) rd[i] = f.pd[i] - st.od[i];
-            cross3(ad, r, t1);
-            cross3(a, rd, t2);
-#pragma unroll
-            for (int i = 0; i < 3; ++i) lin[i] = t1[i] + t2[i];
-            if (rf == 1) {  // d/dt (R^T J_lwa) = R^T (dJ_lwa - w x J_lwa)
-              T jl[3], wl[3], wa[3];
-              cross3(a, r, jl);
-              cross3(f.w, jl, wl);
-              cross3(f.w, a, wa);
-              T l2[3], a2[3];
-#pragma unroll
-              for (int i = 0; i < 3; ++i) {
-                l2[i] = lin[i] - wl[i];
-                a2[i] = ad[i] - wa[i];
-              }
-              to_rf(rf, f, l2, a2, col);
-            } else if (rf == 0) {  // d/dt [o x a; a] = [o' x a + o x a'; a']
-              T t3[3], t4[3];
-              cross3(st.od, a, t3);
-              cross3(st.o, ad, t4);
-#pragma unroll
-              for (int i = 0; i < 3; ++i) {
-                col[i] = t3[i] + t4[i];
-                col[3 + i] = ad[i];
-              }
-            } else {
-              to_rf(rf, f, lin, ad, col);
-            }
-#pragma unroll
-            for (int i = 0; i < 6; ++i) acc[i] += col[i] * vj;
-          }
-          if (dst) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) rows[i * nq + j] = col[i];
-          }
-        }
-        if (want_dJv) {
-          T* out = (T*)o.dJv + p * 12 + arm * 6;
-#pragma unroll
-          for (int i = 0; i < 6; ++i) out[i] = acc[i];
-        }
-      }
-      if (dst) {
-        __syncthreads();
-        tile_store(tile, dst + p0 * per_state, ns * per_state);
-        __syncthreads();
-      }
-    }
+  const size_t lds = (o.J || o.dJ) ? sizeof(T) * kStatesPerTile * 12 * nq : 0;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)ikg_frame_kin_kernel<T, RF, SP>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((ikg_frame_kin_kernel<T, RF, SP>), dim3((unsigned)ntiles), dim3(64), lds, s, dm, q, v, qd, vd,
+                     B, o);
+  return hipGetLastError();
+}
+
+template <typename T, class SP>
+static hipError_t launch_frame_kin_sp(const KModel<T>* dm, int nq, const T* q, const T* v, const T* qd, const T* vd,
+                                      int64_t B, int rf, const FrameKinOut& o, hipStream_t s) {
+  switch (rf) {
+    case 0: return launch_frame_kin_t<T, 0, SP>(dm, nq, q, v, qd, vd, B, o, s);
+    case 1: return launch_frame_kin_t<T, 1, SP>(dm, nq, q, v, qd, vd, B, o, s);
+    default: return launch_frame_kin_t<T, 2, SP>(dm, nq, q, v, qd, vd, B, o, s);
   }
 }
 
 template <typename T>
-hipError_t launch_frame_kin(const KModel<T>* dm, int nq, const void* q, const void* v, const void* qd, const void* vd,
-                            int64_t B, int rf, const FrameKinOut& o, hipStream_t s) {
+hipError_t launch_frame_kin(const KModel<T>* dm, int nq, int spec, const void* q, const void* v, const void* qd,
+                            const void* vd, int64_t B, int rf, const FrameKinOut& o, hipStream_t s) {
   if (B <= 0) return hipSuccess;
-  const int64_t ntiles = (B + kStatesPerTile - 1) / kStatesPerTile;
-  const size_t lds = (o.J || o.dJ) ? sizeof(T) * kStatesPerTile * 12 * nq : 0;
-  // enough workgroups to fill the chip several times over; each zeroes its
-  // LDS tile once and then strides over tiles
-  const int64_t grid = ntiles < 8192 ? ntiles : 8192;
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute((const void*)ikg_frame_kin_kernel<T>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-  }
-  hipLaunchKernelGGL((ikg_frame_kin_kernel<T>), dim3((unsigned)grid), dim3(64), lds, s, dm, (const T*)q,
-                     (const T*)v, (const T*)qd, (const T*)vd, B, rf, o);
-  return hipGetLastError();
+  if ((B + kStatesPerTile - 1) / kStatesPerTile > 0x7fffffff) return hipErrorInvalidValue;
+  const T *tq = (const T*)q, *tv = (const T*)v, *tqd = (const T*)qd, *tvd = (const T*)vd;
+  if (spec == kSpecNextage) return launch_frame_kin_sp<T, SpecNextage>(dm, nq, tq, tv, tqd, tvd, B, rf, o, s);
+  return launch_frame_kin_sp<T, SpecGeneric>(dm, nq, tq, tv, tqd, tvd, B, rf, o, s);
 }
 
-template hipError_t launch_frame_kin<double>(const KModel<double>*, int, const void*, const void*, const void*,
+template hipError_t launch_frame_kin<double>(const KModel<double>*, int, int, const void*, const void*, const void*,
                                              const void*, int64_t, int, const FrameKinOut&, hipStream_t);
-template hipError_t launch_frame_kin<float>(const KModel<float>*, int, const void*, const void*, const void*,
+template hipError_t launch_frame_kin<float>(const KModel<float>*, int, int, const void*, const void*, const void*,
                                             const void*, int64_t, int, const FrameKinOut&, hipStream_t);
 
 }  // namespace ikg

@@ -98,7 +98,8 @@ struct FrameKinOut {
   void* derr;       // [B,12]
 };
 template <typename T>
-hipError_t launch_frame_kin(const KModel<T>* dm, int nq, const void* q, const void* v, const void* qd, const void* vd,
+hipError_t launch_frame_kin(const KModel<T>* dm, int nq, int spec, const void* q, const void* v, const void* qd,
+                            const void* vd,
                             int64_t B, int rf, const FrameKinOut& o, hipStream_t s);
 
 }  // namespace ikg

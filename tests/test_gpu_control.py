@@ -108,3 +108,22 @@ def test_full_size_properties_torch():
     assert ((fd - r["dJ"]).abs() / scale).max().item() < 1e-7
     torch.cuda.synchronize()
     s.close()
+
+
+def test_generic_spec_path(cc):
+    """The runtime-axis / placement-rotation path (SpecGeneric): the same
+    robot with one arm placement rotation perturbed by 1e-300 (no longer the
+    exact identity, so the compiled Nextage specialisation does not apply)."""
+    import copy
+    from ikgrasp.model import load_nextage
+    from ikgrasp.solver import IKSolver
+    m = copy.deepcopy(load_nextage())
+    j = int(m.arm_q[0][2])
+    m.R[j][0, 1], m.R[j][1, 0] = -1e-300, 1e-300
+    s = IKSolver(m, device=0)
+    for rf in (0, 1, 2):
+        r = s.frame_kinematics(cc["q"], cc["v"], cc["q_des"], cc["v_des"], rf=rf, outputs=KEYS + ("err", "derr"))
+        for k in KEYS:
+            np.testing.assert_allclose(r[k], cc[f"{k}_rf{rf}"], rtol=0, atol=1e-11, err_msg=k)
+        np.testing.assert_allclose(r["err"], cc["err"], rtol=0, atol=1e-12)
+    s.close()
