@@ -79,12 +79,17 @@ def main():
     out_bytes = sum(shapes[k] for k in outs) * esz
     per_state = in_bytes + out_bytes
     gbs = per_state * B / (ms * 1e-3) / 1e9
+    traffic = None  # measured HBM bytes per launch (tools/control_pmc.sh), for this exact configuration
+    pmc = os.path.join(ROOT, "profiles", "r01", "control", f"pmc_{a.outputs}_{a.dtype}_b{B}.json")
+    if a.rf == 2 and os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
     line = {
         "bench": "controller kinematics (SURVEY 8f-4): ikg_frame_kinematics_batch",
         "batch": B, "dtype": a.dtype, "rf": a.rf, "outputs": list(outs),
         "ms_per_launch": ms, "states_per_s": B / (ms * 1e-3),
         "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_state": per_state,
+                     "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes_per_state": per_state,
                      "kernel": "ikg_frame_kin_kernel"},
     }
     if not a.no_cpu:
