@@ -128,8 +128,10 @@ def _link_geoms(root, joint_index_of_link):
     return out
 
 
-def _robot_link_frames(root, joint_names):
-    """link -> (q index of its parent joint or -1, link placement in that joint frame)."""
+def _robot_link_frames(root, joint_names, axis_frames=None):
+    """link -> (q index of its parent joint or -1, link placement in that joint frame).
+    axis_frames: the model's joint-frame changes Q (DualArmModel.axis_frames(),
+    non-canonical axes): a revolute joint's child link sits at Q^T in its frame."""
     joints = {j.get("name"): j for j in root.findall("joint")}
     parent_joint = {}
     for j in joints.values():
@@ -143,7 +145,8 @@ def _robot_link_frames(root, joint_names):
         if j is None:
             res = (-1, (np.eye(3), np.zeros(3)))
         elif j.get("type") == "revolute":
-            res = (joint_names.index(j.get("name")), (np.eye(3), np.zeros(3)))
+            q = joint_names.index(j.get("name"))
+            res = (q, (np.eye(3) if axis_frames is None else np.asarray(axis_frames[q]).T, np.zeros(3)))
         else:  # fixed: fold the origin into the parent's frame
             pj, pM = resolve(j.find("parent").get("link"))
             res = (pj, _compose(pM, _origin(j)))
@@ -154,10 +157,11 @@ def _robot_link_frames(root, joint_names):
 
 
 def build_scene(robot_urdf, srdf, table_urdf, obstacle_urdf, cube_urdf, joint_names, robot_placement,
-                table_placement, obstacle_placement, cube_placement) -> CollisionScene:
-    """Placements are (R, t) tuples (config.py:33-37)."""
+                table_placement, obstacle_placement, cube_placement, axis_frames=None) -> CollisionScene:
+    """Placements are (R, t) tuples (config.py:33-37); axis_frames = the
+    robot model's DualArmModel.axis_frames() (identity for the Nextage)."""
     rroot = ET.parse(robot_urdf).getroot()
-    geoms = _link_geoms(rroot, _robot_link_frames(rroot, joint_names))
+    geoms = _link_geoms(rroot, _robot_link_frames(rroot, joint_names, axis_frames))
     # translaterobot: only geometryObjects[0:2] are moved (setup_pinocchio.py:30-31)
     for g in geoms[:2]:
         g.R, g.t = _compose(robot_placement, (g.R, g.t))

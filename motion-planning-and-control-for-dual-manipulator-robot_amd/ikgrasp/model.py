@@ -18,7 +18,17 @@ The kernel's structural contract (checked in `DualArmModel.validate`): one
 shared root joint (the chest) followed by two 6-joint arm chains ending in
 the left/right effector frames; all other joints are passive (never moved by
 the IK, only clamped, as the reference's zero Jacobian columns imply).
-Revolute axes must be +X, +Y or +Z (Pinocchio's RX/RY/RZ joints).
+
+Joint axes (SURVEY §8 row f-3).  +X/+Y/+Z become Pinocchio's RX/RY/RZ joints;
+any other direction e (a negative or tilted axis: Pinocchio's
+RevoluteUnaligned, rotation exp(q [e]x)) is compiled onto the canonical axis c
+nearest to it by re-expressing the joint's frame: with Q c = e,
+Rot(e, q) = Q Rot(c, q) Q^T, so the joint gets placement Q_parent^T P Q and
+axis c, and everything attached to it (child joint placements, frames,
+collision geometries) is premultiplied by Q^T.  World placements of every
+frame and geometry, the joint origins and world axes -- hence FK, every frame
+Jacobian and the IK iterates -- are unchanged, while the kernels keep their
+compile-time canonical-axis rotations.
 """
 from __future__ import annotations
 
@@ -31,7 +41,6 @@ from dataclasses import dataclass, field
 import numpy as np
 
 ARM_DOF = 6
-AXIS_NAMES = {(1.0, 0.0, 0.0): 0, (0.0, 1.0, 0.0): 1, (0.0, 0.0, 1.0): 2}
 
 
 def rpy_to_matrix(r: float, p: float, y: float) -> np.ndarray:
@@ -80,9 +89,36 @@ class Joint:
     parent: int          # parent joint index (-1 = universe), in q order
     R: np.ndarray        # placement in the parent joint frame
     t: np.ndarray
-    axis: int            # 0/1/2 = X/Y/Z
+    axis: int            # 0/1/2 = X/Y/Z: the kernel's canonical axis
     lower: float
     upper: float
+    axis_dir: np.ndarray = None  # the URDF axis, normalised
+    Q: np.ndarray = None         # joint-frame change with Q e_axis = axis_dir (I when aligned)
+
+
+def _unit(k: int) -> np.ndarray:
+    e = np.zeros(3)
+    e[k] = 1.0
+    return e
+
+
+def axis_frame(e: np.ndarray):
+    """(canonical axis code c, rotation Q with Q e_c = e) for a unit axis e:
+    Q = I for +X/+Y/+Z; a half turn about the next canonical axis for -X/-Y/-Z
+    (exact); otherwise the minimal rotation from e_c (c = largest |e_i|) to e."""
+    c = int(np.argmax(np.abs(e)))
+    u = _unit(c)
+    if np.array_equal(e, u):
+        return c, np.eye(3)
+    if np.array_equal(e, -u):
+        Q = -np.eye(3)
+        k = (c + 1) % 3
+        Q[k, k] = 1.0  # rotation by pi about axis k: diag(+1 on k, -1 elsewhere)
+        return c, Q
+    k = np.cross(u, e)
+    s2 = float(k @ k)
+    K = np.array([[0.0, -k[2], k[1]], [k[2], 0.0, -k[0]], [-k[1], k[0], 0.0]])
+    return c, np.eye(3) + K + K @ K * ((1.0 - float(u @ e)) / s2)
 
 
 @dataclass
@@ -143,17 +179,20 @@ def parse_urdf(path_or_xml: str, base_placement=None) -> KinematicTree:
                 tree.frames[child] = Frame(child, parent_joint, origin[0], origin[1])
                 visit(child, parent_joint, origin)
             elif jtype == "revolute":
-                ax = tuple(_floats(j.find("axis").get("xyz") if j.find("axis") is not None else None,
-                                   3, (1.0, 0.0, 0.0)))
-                if ax not in AXIS_NAMES:
-                    raise ValueError(f"joint {jname}: axis {ax} is not +X/+Y/+Z (unsupported)")
+                ax = np.array(_floats(j.find("axis").get("xyz") if j.find("axis") is not None else None,
+                                      3, (1.0, 0.0, 0.0)))
+                nrm = float(np.linalg.norm(ax))
+                if not nrm > 0.0:
+                    raise ValueError(f"joint {jname}: zero axis")
+                e = ax / nrm
+                code, Q = axis_frame(e)
                 lim = j.find("limit")
                 lower = float(lim.get("lower", "0")) if lim is not None else 0.0
                 upper = float(lim.get("upper", "0")) if lim is not None else 0.0
                 R, t = origin
                 if parent_joint < 0 and base_placement is not None:
                     R, t = _compose(base_placement, (R, t))
-                tree.joints.append(Joint(jname, parent_joint, R, t, AXIS_NAMES[ax], lower, upper))
+                tree.joints.append(Joint(jname, parent_joint, R, t, code, lower, upper, e, Q))
                 idx = len(tree.joints) - 1
                 tree.frames[jname] = Frame(jname, idx, np.eye(3), np.zeros(3))
                 tree.frames[child] = Frame(child, idx, np.eye(3), np.zeros(3))
@@ -162,6 +201,15 @@ def parse_urdf(path_or_xml: str, base_placement=None) -> KinematicTree:
                 raise ValueError(f"joint {jname}: type {jtype!r} unsupported by the IK kernel")
 
     visit(roots[0], -1, identity)
+    # re-express every joint frame so that its axis is canonical (module doc):
+    # placement P -> Q_parent^T P Q, anything attached to joint j -> Q_j^T (.)
+    Qs = [jt.Q for jt in tree.joints]
+    for jt in tree.joints:
+        Qp = Qs[jt.parent] if jt.parent >= 0 else np.eye(3)
+        jt.R, jt.t = Qp.T @ jt.R @ jt.Q, Qp.T @ jt.t
+    for f in tree.frames.values():
+        if f.parent >= 0:
+            f.R, f.t = Qs[f.parent].T @ f.R, Qs[f.parent].T @ f.t
     return tree
 
 
@@ -183,6 +231,10 @@ class DualArmModel:
     hook_t: np.ndarray       # [2,3]
     hand_names: tuple = ("LARM_EFF", "RARM_EFF")
     hook_names: tuple = ("LARM_HOOK", "RARM_HOOK")
+    Q: np.ndarray = None     # [nq,3,3] joint-frame changes of non-canonical axes (parse_urdf); I if None
+
+    def axis_frames(self) -> np.ndarray:
+        return np.stack([np.eye(3)] * self.nq) if self.Q is None else self.Q
 
     @property
     def nq(self) -> int:
@@ -238,7 +290,8 @@ class DualArmModel:
             lower=np.array([j.lower for j in robot.joints]), upper=np.array([j.upper for j in robot.joints]),
             root_q=chains[0][0], arm_q=np.array(arms, dtype=np.int32),
             hand_R=hand_R, hand_t=hand_t, hook_R=hook_R, hook_t=hook_t,
-            hand_names=tuple(hands), hook_names=tuple(hooks)).validate()
+            hand_names=tuple(hands), hook_names=tuple(hooks),
+            Q=np.stack([j.Q for j in robot.joints])).validate()
 
     @staticmethod
     def from_urdf(robot_urdf: str, cube_urdf: str, base_placement=None, **kw) -> "DualArmModel":
@@ -254,6 +307,7 @@ class DualArmModel:
             "hand_R": self.hand_R.tolist(), "hand_t": self.hand_t.tolist(),
             "hook_R": self.hook_R.tolist(), "hook_t": self.hook_t.tolist(),
             "hand_names": list(self.hand_names), "hook_names": list(self.hook_names),
+            "Q": self.axis_frames().tolist(),
         }
         return json.dumps(d, indent=1)
 
@@ -267,7 +321,8 @@ class DualArmModel:
             root_q=d["root_q"], arm_q=np.array(d["arm_q"], dtype=np.int32),
             hand_R=np.array(d["hand_R"]), hand_t=np.array(d["hand_t"]),
             hook_R=np.array(d["hook_R"]), hook_t=np.array(d["hook_t"]),
-            hand_names=tuple(d["hand_names"]), hook_names=tuple(d["hook_names"])).validate()
+            hand_names=tuple(d["hand_names"]), hook_names=tuple(d["hook_names"]),
+            Q=np.array(d["Q"]) if "Q" in d else None).validate()
 
 
 DATA_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")

@@ -33,6 +33,14 @@
    states are those plus a seeded tracking error, plus 32 random states within
    the joint limits; outputs are the frame placements, velocities, J, dJ, dJ v
    in WORLD / LOCAL / LOCAL_WORLD_ALIGNED and the PD errors e, e_dot.
+8. `tilted_cube.urdf` + `generic_cases.npz` — the model-generality row (SURVEY
+   §8f-3) on the synthetic tilted-axis robot `tilted_dualarm.urdf` (negative
+   and unaligned joint axes, rotated placements; written for these tests):
+   the cube's hook frames are the robot's hand frames at a fixed grasp posture
+   q*, seen from a cube placed between the hands; fixtures are IK solves by
+   oracle/generic_oracle.py (raw-axis Rodrigues restatement, itself checked
+   against KAT-1/2 on the reference URDF here) from q = 0 and from perturbed
+   q*, plus FK / LOCAL Jacobians / geometry placements at random q.
 """
 import json
 import os
@@ -298,8 +306,87 @@ def make_control_cases(n_times=24, n_random=32):
     print("wrote control_cases.npz:", len(q), "states")
 
 
+Q_STAR = np.array([0.0, 0.0, 0.2, -0.3, -1.4, 0.1, 0.3, 0.2, -0.2, -0.3, -1.4, -0.1, -0.3, -0.2])
+
+
+def _rpy(R):
+    """URDF rpy of a rotation (R = Rz(y) Ry(p) Rx(r))."""
+    return np.arctan2(R[2, 1], R[2, 2]), np.arcsin(-R[2, 0]), np.arctan2(R[1, 0], R[0, 0])
+
+
+def _generic_solve(args):
+    from oracle import generic_oracle as go
+    tg, q0 = args
+    m = go.ChainModel(os.path.join(HERE, "tilted_dualarm.urdf"))
+    hooks = go.cube_hooks(os.path.join(HERE, "tilted_cube.urdf"))
+    q, ok, it, e = go.computeqgrasppose(m, hooks, q0, tg[:9].reshape(3, 3), tg[9:])
+    return q, ok, it, e
+
+
+def make_generic_cases(n_cold=24, n_warm=24, n_fk=32):
+    from oracle import generic_oracle as go
+    from oracle import ik_oracle as ik
+    if os.path.isdir(REF):  # pin the generic restatement on the reference URDF (KAT-1/2)
+        kat = json.load(open(os.path.join(HERE, "kat.json")))
+        m = go.ChainModel(os.path.join(REF, "models/nextagea_description/urdf/NextageaOpen.urdf"),
+                          (np.eye(3), np.array([0.0, 0.0, 0.85])))
+        hooks = go.cube_hooks(os.path.join(REF, "models/cubes/cube_small.urdf"))
+        for key, qk, n in (("cube_placement", "q0", 740), ("cube_placement_target", "qe", 736)):
+            q, ok, it, _ = go.computeqgrasppose(m, hooks, np.zeros(15), np.array(kat[key]["R"]), np.array(kat[key]["t"]))
+            assert ok and it == n and np.abs(q - np.array(kat[qk])).max() < 1e-14, (key, it)
+    robot = go.ChainModel(os.path.join(HERE, "tilted_dualarm.urdf"))
+    oMi = robot.fk(Q_STAR)
+    hands = [robot.frame(oMi, h) for h in ("LARM_EFF", "RARM_EFF")]
+    center = 0.5 * (hands[0][1] + hands[1][1])
+    lines = ['<?xml version="1.0"?>',
+             '<!-- Grasp object of the synthetic tilted-axis robot (tests/golden/make_golden.py generic):',
+             '     hook frames = the hands at the posture Q_STAR seen from a cube frame between them. -->',
+             '<robot name="tilted_cube">', '  <link name="base_link"/>']
+    for h, (R, t) in zip(("LARM_HOOK", "RARM_HOOK"), hands):
+        r, p_, y = (float(x) for x in _rpy(R))
+        d = [float(x) for x in t - center]
+        lines += [f'  <link name="{h}_link"/>',
+                  f'  <joint name="{h}" type="fixed"><parent link="base_link"/><child link="{h}_link"/>',
+                  f'    <origin xyz="{d[0]!r} {d[1]!r} {d[2]!r}" rpy="{r!r} {p_!r} {y!r}"/></joint>']
+    lines.append("</robot>")
+    with open(os.path.join(HERE, "tilted_cube.urdf"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    rng = np.random.default_rng(41)
+    n = n_cold + n_warm
+    targets = np.zeros((n, 12))
+    for i in range(n):
+        yaw = rng.uniform(-0.25, 0.25)
+        c, s_ = np.cos(yaw), np.sin(yaw)
+        targets[i, :9] = np.array([[c, -s_, 0], [s_, c, 0], [0, 0, 1]]).reshape(9)
+        targets[i, 9:] = center + rng.uniform(-0.05, 0.05, 3)
+    q0 = np.zeros((n, robot.nq))
+    q0[n_cold:] = Q_STAR + rng.normal(scale=0.1, size=(n_warm, robot.nq))
+    q0[n_cold:, 1] = 0.0
+    with Pool(8) as p:
+        res = p.map(_generic_solve, list(zip(targets, q0)))
+    q_fk = rng.uniform(robot.lower, robot.upper, size=(n_fk, robot.nq))
+    fk_hands, fk_J, geo_names, geo = [], [], None, []
+    for q in q_fk:
+        o = robot.fk(q)
+        fk_hands.append([np.concatenate([robot.frame(o, h)[0].reshape(9), robot.frame(o, h)[1]])
+                         for h in ("LARM_EFF", "RARM_EFF")])
+        fk_J.append(np.vstack([robot.frame_jacobian_local(q, h, o) for h in ("LARM_EFF", "RARM_EFF")]))
+        g = robot.geometry_placements(o)
+        geo_names = sorted(g)
+        geo.append([np.concatenate([g[k][0].reshape(9), g[k][1]]) for k in geo_names])
+    np.savez_compressed(
+        os.path.join(HERE, "generic_cases.npz"), q_star=Q_STAR, targets=targets, q0=q0,
+        q=np.array([r[0] for r in res]), converged=np.array([r[1] for r in res]),
+        iters=np.array([r[2] for r in res], dtype=np.int32), err=np.array([r[3] for r in res]),
+        fk_q=q_fk, fk_hands=np.array(fk_hands), fk_J=np.array(fk_J), geo_names=np.array(geo_names),
+        geo=np.array(geo))
+    conv = np.array([r[1] for r in res])
+    print("wrote tilted_cube.urdf, generic_cases.npz:", int(conv[:n_cold].sum()), "/", n_cold, "cold,",
+          int(conv[n_cold:].sum()), "/", n_warm, "warm converged; iters", [r[2] for r in res][:8])
+
+
 if __name__ == "__main__":
-    what = sys.argv[1:] or ["kat", "cases", "scene", "collision", "collision_solve", "planner", "control"]
+    what = sys.argv[1:] or ["kat", "cases", "scene", "collision", "collision_solve", "planner", "control", "generic"]
     if os.path.isdir(REF) and "kat" in what:
         make_kats()
     if "cases" in what:
@@ -314,3 +401,5 @@ if __name__ == "__main__":
         make_planner_cases()
     if os.path.isdir(REF) and "control" in what:
         make_control_cases()
+    if "generic" in what:
+        make_generic_cases()

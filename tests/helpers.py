@@ -61,3 +61,25 @@ def hand_errors_from_fk(model, hands, targets):
         th = hands[:, h, 9:].astype(np.float64)
         out[:, h] = se3_err(Rh, th, TR[:, h], Tt[:, h])
     return out
+
+
+def fk_tables(model, q):
+    """FK of compiled model tables (canonical joint axes; DualArmModel): joint
+    frames [(R, t)] in q order.  Test infrastructure (numpy)."""
+    from oracle import ik_oracle as ik
+    oMi = []
+    for j in range(model.nq):
+        liMi = (model.R[j] @ ik.axis_rotation(int(model.axis[j]), q[j]), model.t[j])
+        oMi.append(liMi if model.parents[j] < 0 else ik.se3_mul(oMi[model.parents[j]], liMi))
+    return oMi
+
+
+def hands_from_tables(model, q):
+    """[2,12] hand placements from compiled tables."""
+    from oracle import ik_oracle as ik
+    oMi = fk_tables(model, q)
+    out = []
+    for h in range(2):
+        R, t = ik.se3_mul(oMi[int(model.arm_q[h][-1])], (model.hand_R[h], model.hand_t[h]))
+        out.append(np.concatenate([R.reshape(9), t]))
+    return np.array(out)

@@ -57,10 +57,12 @@ def test_urdf_children_sorted_by_joint_name():
     assert tree.joints[0].axis == 0 and tree.joints[1].axis == 1
 
 
-def test_unsupported_axis_rejected():
-    bad = TOY.replace('<axis xyz="0 1 0"/>', '<axis xyz="0 0.6 0.8"/>')
-    with pytest.raises(ValueError, match="axis"):
-        parse_urdf(bad)
+def test_unaligned_axis_compiled_onto_canonical_axis():
+    """An unaligned axis (RevoluteUnaligned) is re-expressed on the nearest
+    canonical axis (here Z); tests/test_generic_model.py checks the kinematics."""
+    tree = parse_urdf(TOY.replace('<axis xyz="0 1 0"/>', '<axis xyz="0 0.6 0.8"/>'))
+    j = tree.joints[1]
+    assert j.axis == 2 and np.allclose(j.Q @ np.array([0, 0, 1.0]), [0, 0.6, 0.8])
 
 
 def test_structure_validation_rejects_non_dual_arm():

@@ -37,7 +37,7 @@ def main(ref="/root/reference"):
         cube, m.joint_names, base,
         (rotate("z", -np.pi / 2), np.array([0.8, 0.0, 0.0])),
         (rotate("z", 0.0), np.array([0.43, -0.1, 0.94])),
-        (rotate("z", 0.0), np.array([0.33, -0.3, 0.93])))
+        (rotate("z", 0.0), np.array([0.33, -0.3, 0.93])), axis_frames=m.axis_frames())
     with open(NEXTAGE_COLLISION_JSON, "w") as f:
         f.write(scene.to_json())
     print(f"wrote {NEXTAGE_COLLISION_JSON}: {len(scene.geoms)} geometries, {len(scene.pairs)} pairs")
