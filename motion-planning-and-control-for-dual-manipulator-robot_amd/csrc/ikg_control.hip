@@ -38,6 +38,15 @@ namespace {
 #define IKG_FK_TILE 32
 #endif
 constexpr int kStatesPerTile = IKG_FK_TILE;
+// LDS holds the dense matrices of one slice of the tile at a time and the
+// emission pass runs once per slice.  fp64: two slices of 16 states (23 KB,
+// 6 workgroups per CU instead of 3) -- measured -18% for the task_space_terms
+// output set, -3% for all outputs, +1% for J + dJ; fp32 (23 KB for 32 states
+// already): one slice (two measured +6%).
+template <typename T>
+constexpr int slices() {
+  return sizeof(T) == 8 ? 2 : 1;
+}
 
 template <typename T>
 __device__ inline void cross3(const T* a, const T* b, T* c) {
@@ -367,6 +376,8 @@ __global__ __launch_bounds__(64) void ikg_frame_kin_kernel(const KModel<T>* __re
                                                            const T* __restrict__ vd, int64_t B, FrameKinOut o) {
   extern __shared__ __align__(16) unsigned char smem[];
   T* tile = reinterpret_cast<T*>(smem);
+  constexpr int kSlices = slices<T>();
+  constexpr int kSliceStates = kStatesPerTile / kSlices;
   const int nq = m->nq;
   const int per_state = 12 * nq;
   const int lane = threadIdx.x;
@@ -378,7 +389,7 @@ __global__ __launch_bounds__(64) void ikg_frame_kin_kernel(const KModel<T>* __re
   const bool live = sl < ns;
   const int64_t p = p0 + sl;
   if (o.J || o.dJ) {
-    for (int i = lane; i < kStatesPerTile * per_state; i += 64) tile[i] = T(0);
+    for (int i = lane; i < kSliceStates * per_state; i += 64) tile[i] = T(0);  // once: same non-zeros every slice
   }
   JointVals<T> jv;
   FramePass<T> f;
@@ -425,24 +436,33 @@ __global__ __launch_bounds__(64) void ikg_frame_kin_kernel(const KModel<T>* __re
       }
     }
   }
-  T* rows = tile + sl * per_state + 6 * arm * nq;
+  T* rows = tile + (sl % kSliceStates) * per_state + 6 * arm * nq;
   if (o.J) {
-    if (live) emit_columns<0, RF, SP>(m, right, jv, f, rows, nq, (T*)nullptr);
-    __syncthreads();
-    tile_store(tile, (T*)o.J + p0 * per_state, ns * per_state);
-    __syncthreads();
+#pragma unroll 1
+    for (int h = 0; h < kSlices; ++h) {
+      if (live && sl / kSliceStates == h) emit_columns<0, RF, SP>(m, right, jv, f, rows, nq, (T*)nullptr);
+      __syncthreads();
+      const int nsh = min(max(ns - h * kSliceStates, 0), kSliceStates);
+      tile_store(tile, (T*)o.J + (p0 + h * kSliceStates) * per_state, nsh * per_state);
+      __syncthreads();
+    }
   }
   if (o.dJ || o.dJv) {
     T acc[6] = {T(0), T(0), T(0), T(0), T(0), T(0)};
-    if (live) emit_columns<1, RF, SP>(m, right, jv, f, rows, nq, acc);
+#pragma unroll 1
+    for (int h = 0; h < kSlices; ++h) {
+      if (live && sl / kSliceStates == h) emit_columns<1, RF, SP>(m, right, jv, f, rows, nq, acc);
+      if (o.dJ) {
+        __syncthreads();
+        const int nsh = min(max(ns - h * kSliceStates, 0), kSliceStates);
+        tile_store(tile, (T*)o.dJ + (p0 + h * kSliceStates) * per_state, nsh * per_state);
+        if (h + 1 < kSlices) __syncthreads();
+      }
+    }
     if (live && o.dJv) {
       T* out = (T*)o.dJv + p * 12 + arm * 6;
 #pragma unroll
       for (int i = 0; i < 6; ++i) out[i] = acc[i];
-    }
-    if (o.dJ) {
-      __syncthreads();
-      tile_store(tile, (T*)o.dJ + p0 * per_state, ns * per_state);
     }
   }
 }
@@ -451,7 +471,7 @@ template <typename T, int RF, class SP>
 static hipError_t launch_frame_kin_t(const KModel<T>* dm, int nq, const T* q, const T* v, const T* qd, const T* vd,
                                      int64_t B, const FrameKinOut& o, hipStream_t s) {
   const int64_t ntiles = (B + kStatesPerTile - 1) / kStatesPerTile;
-  const size_t lds = (o.J || o.dJ) ? sizeof(T) * kStatesPerTile * 12 * nq : 0;
+  const size_t lds = (o.J || o.dJ) ? sizeof(T) * (kStatesPerTile / slices<T>()) * 12 * nq : 0;
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)ikg_frame_kin_kernel<T, RF, SP>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
