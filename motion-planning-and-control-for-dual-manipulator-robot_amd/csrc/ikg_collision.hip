@@ -25,6 +25,11 @@ namespace ikg {
 // phase; totals are summed into g_cprof.
 #ifdef IKG_CPROF
 __device__ unsigned long long g_cprof[8];
+// certificate statistics: checks run, checks answered by the certificate,
+// tetrahedra available on a hit, EPA attempts, EPA certificates, sum of
+// certified margins (nm)
+__device__ unsigned long long g_skip[6];
+#define SKIP_STAT(i, v) atomicAdd(&g_skip[i], (unsigned long long)(v))
 // `cp_lead` (in scope at every use): this lane accumulates for its problem
 #define CPROF_MARK(acc, t)                   \
   do {                                       \
@@ -37,6 +42,9 @@ __device__ unsigned long long g_cprof[8];
     if (prof && cp_lead) prof[i] += v; \
   } while (0)
 #else
+#define SKIP_STAT(i, v) \
+  do {                  \
+  } while (0)
 #define CPROF_MARK(acc, t) \
   do {                     \
   } while (0)
@@ -307,6 +315,40 @@ __device__ inline GroupLds<T> group_view(char* base, int g, int nq, int ng) {
   return v;
 }
 
+// Penetration certificate of the witness pair (one lane; rare, so kept out of
+// line: inlined, its temporaries raised the register pressure of the whole
+// continuation loop).  EPA lower bound on the depth minus the placement
+// rounding of the I/O type; per joint j, the lever-arm bound Rmot[j] of the two
+// geometries about it (distance of the geometry's centre from the joint origin
+// + its bounding radius + twice the margin, which bounds that distance over the
+// motions the margin allows).
+template <typename T>
+__device__ __attribute__((noinline)) void certify_witness(int nq, Shape<T> A, Shape<T> B, Witness<T>& W,
+                                                          const T (*Fa)[12], const int32_t* par) {
+  const double tol = sizeof(T) == 8 ? 1e-9 : 1e-5;
+  const double d = epa_depth_lb(A, B, W.pts, W.epa) - tol;
+  SKIP_STAT(3, 1);
+  if (!(d > 0.0)) {
+    W.epa_wait = 32;
+    return;
+  }
+  SKIP_STAT(4, 1);
+  SKIP_STAT(5, d * 1e9);
+  for (int j = 0; j < nq; ++j) W.Rmot[j] = T(0);
+  for (int g = 0; g < 2; ++g) {
+    if (W.gtarget[g]) continue;
+    const T* c = W.P[g] + 9;
+    for (int j = W.gjoint[g]; j >= 0; j = par[j]) {
+      const T dx = c[0] - Fa[j][9], dy = c[1] - Fa[j][10], dz = c[2] - Fa[j][11];
+      W.Rmot[j] += sqrt(dx * dx + dy * dy + dz * dz) + W.gbrad[g] + T(2.0 * d);
+    }
+  }
+  W.budget = d;
+  W.Emot = 0.0;
+  W.skip_ok = 1;
+  ++W.gen;
+}
+
 // One collision check for every group with `need` set (group-uniform); all 64
 // lanes call it.  Joint frames come from the IK lanes' FK of the same iterate
 // (fk_arm WANT_FRAMES), so only the passive joints are composed here; then
@@ -367,16 +409,25 @@ __device__ bool collide_group(const KModel<T>* __restrict__ m, const KCollision<
   __syncthreads();
   if (has_w && li == 0) {
     int r = 0;
+    bool tetra = false;  // W.pts hold an origin-enclosing tetrahedron of this iterate
     if (cert && tetra_encloses_origin(W.pts[0], W.pts[1], W.pts[2], W.pts[3])) {
       r = 1;
+      tetra = true;
     } else {
       T cd[12];
       r = pair_collides(A, B, cd);
       W.cert_ok = r == 2;
-      if (r == 2)
+      if (r == 2) {
         for (int i = 0; i < 12; ++i) W.dir[i] = cd[i];
+        for (int k = 0; k < 4; ++k) mink_support(A, B, W.dir + 3 * k, W.pts[k]);
+        tetra = tetra_encloses_origin(W.pts[0], W.pts[1], W.pts[2], W.pts[3]);
+      }
     }
     V.flag[1] = r ? T(1) : T(0);
+    if (r && tetra) SKIP_STAT(2, 1);
+    // penetration certificate: while the accumulated motion bound stays below
+    // it, later checks of this problem are answered without running them
+    if (r && tetra && !W.skip_ok && --W.epa_wait <= 0) certify_witness<T>(m->nq, A, B, W, Fa, V.par);
   }
   __syncthreads();
   bool hit = has_w && V.flag[1] != T(0);
@@ -404,6 +455,9 @@ __device__ bool collide_group(const KModel<T>* __restrict__ m, const KCollision<
     if (sweep && li == 0) {
       W.pair = wnew;
       W.cert_ok = 0;
+      if (W.skip_ok) ++W.gen;
+      W.skip_ok = 0;
+      W.epa_wait = 0;
     }
     if (sweep && found && li < 2) {  // cache the new witness's geometry constants
       const int g = c->pairs[wnew][li];
@@ -413,12 +467,56 @@ __device__ bool collide_group(const KModel<T>* __restrict__ m, const KCollision<
       for (int i = 0; i < 9; ++i) W.gR[li][i] = c->R[g][i];
       for (int i = 0; i < 3; ++i) W.gt[li][i] = c->t[g][i];
       for (int i = 0; i < 3; ++i) W.gdims[li][i] = c->dims[g][i];
+      W.gbrad[li] = c->brad[g];
     }
     if (sweep) hit = found;
     CPROF_MARK(a_sw, t);
     CPROF_ADD(2, a_sw);
   }
   return hit;
+}
+
+// One continuation iteration's FK + errors + step of this lane's arm
+// (inverse_geometry.py:58-83; the IK lanes' frames go to F for the check).
+// Returns the squared error norm of the lane's hand.
+template <typename T, bool DAMPED, class SP>
+__device__ __forceinline__ T cont_step(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, const T* sn,
+                                       const T* cs, const T* RT, const T* tT, T (*F)[12], T* dq, T& s) {
+  ArmState<T> st;
+  const T x = arm_fk_error<T, SP, true>(m, arm, sn, cs, RT, tT, st, F);
+  T alpha, beta;
+  if constexpr (!DAMPED) {
+    T u[6], v[6];
+    arm_solve<T, SP>(st, u, v, alpha, beta);
+    s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+    arm_dq(u, v, s, dq);
+  } else {
+    T A[6][8], ze[6], zc[6];
+    arm_system(st, A);
+    arm_solve_damped(A, prm.lambda, ze, zc, alpha, beta);
+    s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+    arm_dq_damped(A, ze, zc, s, dq);
+  }
+  return x;
+}
+
+// q <- clip(q + dt dq) (:86-89), the certificate's motion bound
+// sum_j |dq_j| Rmot[j] over the root and the lane's arm joints, the trig state.
+template <typename T>
+__device__ __forceinline__ void cont_update(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, T s,
+                                            const T* dq, int it, bool cert_live, const T* Rr, T& emot, T& qc, T* qa,
+                                            T* sn, T* cs) {
+  T q_old[7];
+  q_old[0] = qc;
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
+  arm_update(m, arm, prm.dt, s, dq, qc, qa);
+  if (cert_live) {
+    emot += fabs(qc - q_old[0]) * Rr[0];
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) emot += fabs(qa[k] - q_old[k + 1]) * Rr[k + 1];
+  }
+  trig_advance(qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);
 }
 
 template <typename T, bool DAMPED, class SP, int G>
@@ -429,7 +527,8 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
                                                                   T* __restrict__ q_out,
                                                                   uint8_t* __restrict__ conv,
                                                                   int32_t* __restrict__ iters,
-                                                                  T* __restrict__ err) {
+                                                                  T* __restrict__ err,
+                                                                  const int32_t* __restrict__ witness) {
   extern __shared__ __align__(16) char lds[];
   constexpr int LG = 64 / G;
   const int lane = threadIdx.x;
@@ -438,8 +537,9 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
   const int nq = m->nq;
   const GroupLds<T> V = group_view<T>(lds, g, nq, c->n_geoms);
   const int64_t p = (int64_t)blockIdx.x * G + g;
-  // problems whose hand errors passed in the pair kernel (group-uniform)
-  const bool started = p < B && conv[p] != 0;
+  // problems whose hand errors passed in the pair kernel and whose first
+  // check collided (ikg_prescreen_kernel: the others are final, success)
+  const bool started = p < B && conv[p] != 0 && witness[p] >= 0;
   if (!__any(started)) return;  // whole wave
   bool active = started;
   if (active) {
@@ -452,9 +552,26 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
       V.par[j] = m->jparent[j];
     }
     if (li < 12) V.tgt[li] = targets[t_idx * 12 + li];
+    if (li < 2) {  // the pre-screen's colliding pair is the first witness
+      const int w = witness[p];
+      const int gg = c->pairs[w][li];
+      Witness<T>& W = *V.W;
+      W.gjoint[li] = c->joint[gg];
+      W.gkind[li] = c->kind[gg];
+      W.gtarget[li] = gg == c->target_geom;
+      for (int i = 0; i < 9; ++i) W.gR[li][i] = c->R[gg][i];
+      for (int i = 0; i < 3; ++i) W.gt[li][i] = c->t[gg][i];
+      for (int i = 0; i < 3; ++i) W.gdims[li][i] = c->dims[gg][i];
+      W.gbrad[li] = c->brad[gg];
+    }
     if (li == 0) {
-      V.W->pair = -1;
+      V.W->pair = witness[p];
       V.W->cert_ok = 0;
+      V.W->skip_ok = 0;
+      V.W->epa_wait = 0;
+      V.W->gen = 0;
+      V.W->budget = 0.0;
+      V.W->Emot = 0.0;
     }
   }
   __syncthreads();
@@ -477,53 +594,99 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
 #else
   unsigned long long* prof = nullptr;
 #endif
+  // the IK lanes' copy of the penetration certificate (Witness gen / skip_ok /
+  // budget / Rmot of their chain joints) and the motion bound accumulated
+  // against it, in registers: no LDS traffic per iteration but one int read
+  int cgen = 0;
+  bool cert_live = false;
+  T Rr[7] = {};
+  T emot = T(0), cbudget = T(0);
   for (;;) {
 #ifdef IKG_CPROF
     cp_lead = li == 0 && active;
 #endif
+    // Certified stretch: while the witness pair provably intersects, the
+    // reference's stop test cannot pass, so the IK lanes iterate alone at the
+    // batch kernel's pace (no LDS flags, no barriers).  They leave at the
+    // first iterate whose errors pass once the margin is spent (the loop below
+    // redoes that iterate and runs a real check) or at max_iters.
+    if (active && li < 2 && cert_live && passive_clamped) {
+      for (;;) {
+        if (it >= prm.max_iters) break;
+        T dq[6], s;
+        const T x = cont_step<T, DAMPED, SP>(m, prm, arm, sn, cs, RT, tT, V.F, dq, s);
+        const T xo = pair_swap(x);
+        if (x < prm.eps2 && xo < prm.eps2) {
+          if (!(emot + pair_swap(emot) < cbudget)) break;
+          if (li == 0) SKIP_STAT(1, 1);
+        }
+        cont_update(m, prm, arm, s, dq, it, cert_live, Rr, emot, qc, qa, sn, cs);
+        ++it;
+      }
+      if (arm == 0) V.q[m->root_q] = qc;
+      for (int k = 0; k < kArmDof; ++k) V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
+    }
+    __syncthreads();
     // FK + errors at the current iterate (:58-67) and, before the collision
     // check, the update it would take (:75-83): the Jacobian state dies here,
     // so only q, dq and the trig state stay live across the check
     T dq[6], s = T(0);
     if (active && li < 2) {
-      ArmState<T> st;
-      nrm = arm_fk_error<T, SP, true>(m, arm, sn, cs, RT, tT, st, V.F);  // squared
+      nrm = cont_step<T, DAMPED, SP>(m, prm, arm, sn, cs, RT, tT, V.F, dq, s);
       const T other = pair_swap(nrm);
       if (li == 0) V.flag[0] = (nrm < prm.eps2 && other < prm.eps2) ? T(1) : T(0);
-      T alpha, beta;
-      if constexpr (!DAMPED) {
-        T u[6], v[6];
-        arm_solve<T, SP>(st, u, v, alpha, beta);
-        s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
-        arm_dq(u, v, s, dq);
-      } else {
-        T A[6][8], ze[6], zc[6];
-        arm_system(st, A);
-        arm_solve_damped(A, prm.lambda, ze, zc, alpha, beta);
-        s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
-        arm_dq_damped(A, ze, zc, s, dq);
+      if (V.W->gen != cgen) {  // only invalidations reach here (passive clamp): drop it
+        cgen = V.W->gen;
+        cert_live = false;
       }
+      // collision(q) is known True while the motion bound stays below the margin
+      const T tot = emot + pair_swap(emot);
+      if (li == 0) V.flag[2] = (cert_live && tot < cbudget) ? T(1) : T(0);
     }
     __syncthreads();
     CPROF_MARK(a_fk, t);
     if (active && it >= prm.max_iters) active = false;  // loop exhausted: success stays false
     const bool need = active && V.flag[0] != T(0);
-    if (__any(need)) {
-      const bool col = collide_group<T, LG>(m, c, V, li, lane0, need, gmask, prof);
-      if (need && !col) {
+    // the witness pair provably still intersects (certified margin not yet
+    // used up by the motion bound): collision(q) is True without a check
+    const bool known = need && V.flag[2] != T(0);
+    if (need && !known && li == 0 && V.W->skip_ok) {  // spent: check, then certify afresh
+      V.W->skip_ok = 0;
+      V.W->epa_wait = 0;
+      ++V.W->gen;
+    }
+    const bool check = need && !known;
+    if (li == 0 && check) SKIP_STAT(0, 1);
+    if (li == 0 && known) SKIP_STAT(1, 1);
+    if (__any(check)) {
+      const bool col = collide_group<T, LG>(m, c, V, li, lane0, check, gmask, prof);
+      if (check && !col) {
         success = true;  // :70 errors pass and no collision
         active = false;
       }
     }
     CPROF_MARK(a_col, t);
+    if (__any(check)) __syncthreads();  // collide_group's last witness / certificate writes
+    if (active && li < 2 && V.W->gen != cgen) {
+      // certificate (re)made or dropped at this iterate's check: reload it; the
+      // bound counts the motion from this iterate on
+      cgen = V.W->gen;
+      cert_live = V.W->skip_ok != 0;
+      emot = T(0);
+      if (cert_live) {
+        cbudget = T(V.W->budget);
+        Rr[0] = arm == 0 ? V.W->Rmot[m->root_q] : T(0);  // the root is counted once (left lane)
+        for (int k = 0; k < kArmDof; ++k) Rr[k + 1] = V.W->Rmot[arm ? m->arm_q[1][k] : m->arm_q[0][k]];
+      }
+    }
     if (active && li < 2) {  // apply the update (:86-89)
-      T q_old[7];
-      q_old[0] = qc;
-      for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
-      arm_update(m, arm, prm.dt, s, dq, qc, qa);
-      trig_advance(qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);
+      cont_update(m, prm, arm, s, dq, it, cert_live, Rr, emot, qc, qa, sn, cs);
       if (arm == 0) V.q[m->root_q] = qc;
       for (int k = 0; k < kArmDof; ++k) V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
+    }
+    if (active && !passive_clamped && li == 0 && V.W->skip_ok) {  // the passive joints may move: drop it
+      V.W->skip_ok = 0;
+      ++V.W->gen;
     }
     if (active && !passive_clamped) {  // projecttojointlimits on every joint after the first update
       for (int i = li; i < m->n_passive; i += LG) {
@@ -564,6 +727,41 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
   }
 }
 
+// First check of the collision continuation for every problem whose errors
+// passed (inverse_geometry.py:70), one wave per problem (64 lanes per sweep,
+// against 16 in the continuation's groups): collision-free ones are final
+// (success); for colliding ones the colliding pair found seeds the
+// continuation's witness.  witness[p] = that pair, -1 if none / not converged.
+template <typename T>
+__global__ __launch_bounds__(64) void ikg_prescreen_kernel(const KModel<T>* __restrict__ m,
+                                                           const KCollision<T>* __restrict__ c,
+                                                           const T* __restrict__ q, const T* __restrict__ targets,
+                                                           int64_t S_per_target, int64_t B,
+                                                           const uint8_t* __restrict__ conv,
+                                                           int32_t* __restrict__ witness) {
+  __shared__ CollideScratch<T> S;
+  __shared__ T tgt[12];
+  __shared__ Witness<T> W;
+  const int64_t p = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (!conv[p]) {  // wave-uniform
+    if (lane == 0) witness[p] = -1;
+    return;
+  }
+  const int64_t t_idx = S_per_target > 1 ? p / S_per_target : p;
+  if (lane < m->nq) S.q[lane] = q[p * m->nq + lane];
+  if (lane < 12) tgt[lane] = targets[t_idx * 12 + lane];
+  if (lane == 0) {
+    W.pair = -1;
+    W.cert_ok = 0;
+  }
+  __syncthreads();
+  stage_trig_par(m, S);
+  __syncthreads();
+  const bool col = collide_wave<T, true>(m, c, S, tgt, W);
+  if (lane == 0) witness[p] = col ? W.pair : -1;
+}
+
 // ------------------------------------------------------------------ launchers
 template <typename T>
 hipError_t launch_collision(const KModel<T>* dm, const KCollision<T>* dc, const void* q, const void* targets,
@@ -586,42 +784,59 @@ static int cont_groups() {
 
 template <typename T, bool DAMPED, class SP, int G>
 static void launch_continue_g(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
-                              const BatchArgs& a, int nq, int ng, hipStream_t s) {
+                              const BatchArgs& a, int nq, int ng, const int32_t* wit, hipStream_t s) {
   const size_t lds = (size_t)G * group_lds_bytes<T>(nq, ng);
   hipLaunchKernelGGL((ikg_collide_continue_kernel<T, DAMPED, SP, G>), dim3((unsigned)((a.B + G - 1) / G)), dim3(64),
                      lds, s, dm, dc, prm, (const T*)a.targets, a.S, a.B, (T*)a.q_out, a.converged, a.iters,
-                     (T*)a.err_out);
+                     (T*)a.err_out, wit);
 }
 
 template <typename T, bool DAMPED, class SP>
 static void launch_continue_t(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
-                              const BatchArgs& a, int nq, int ng, hipStream_t s) {
+                              const BatchArgs& a, int nq, int ng, const int32_t* wit, hipStream_t s) {
   if (cont_groups() == 1)
-    launch_continue_g<T, DAMPED, SP, 1>(dm, dc, prm, a, nq, ng, s);
+    launch_continue_g<T, DAMPED, SP, 1>(dm, dc, prm, a, nq, ng, wit, s);
   else
-    launch_continue_g<T, DAMPED, SP, 4>(dm, dc, prm, a, nq, ng, s);
+    launch_continue_g<T, DAMPED, SP, 4>(dm, dc, prm, a, nq, ng, wit, s);
 }
 
 template <typename T>
 hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
                                    const BatchArgs& a, int spec, int nq, int ng, hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
+  if (a.B > 0x7fffffff) return hipErrorInvalidValue;
+  // stream-ordered workspace: the pre-screen's witness pair per problem
+  int32_t* wit = nullptr;
+  hipError_t e = hipMallocAsync((void**)&wit, sizeof(int32_t) * a.B, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
+                     (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, wit);
   const bool damped = prm.lambda > T(0);
   if (spec == kSpecNextage) {
     if (damped)
-      launch_continue_t<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, s);
+      launch_continue_t<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, wit, s);
     else
-      launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, nq, ng, s);
+      launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, nq, ng, wit, s);
   } else {
     if (damped)
-      launch_continue_t<T, true, SpecGeneric>(dm, dc, prm, a, nq, ng, s);
+      launch_continue_t<T, true, SpecGeneric>(dm, dc, prm, a, nq, ng, wit, s);
     else
-      launch_continue_t<T, false, SpecGeneric>(dm, dc, prm, a, nq, ng, s);
+      launch_continue_t<T, false, SpecGeneric>(dm, dc, prm, a, nq, ng, wit, s);
   }
-  return hipGetLastError();
+  e = hipGetLastError();
+  const hipError_t ef = hipFreeAsync(wit, s);
+  return e != hipSuccess ? e : ef;
 }
 
 #ifdef IKG_CPROF
+extern "C" int ikg_debug_skip(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_skip), sizeof(g_skip)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[6] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_skip), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
 extern "C" int ikg_debug_cprof(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cprof), sizeof(g_cprof)) != hipSuccess) return -1;
   if (reset) {

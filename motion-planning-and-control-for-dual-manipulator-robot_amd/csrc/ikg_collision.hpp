@@ -46,12 +46,36 @@ struct CollideScratch {
   T P[kMaxGeoms][12];  // world geometry placements
 };
 
+// Expanding-polytope scratch (epa_depth_lb): at most kEpaIters expansions of
+// the starting tetrahedron.
+constexpr int kEpaIters = 5;
+constexpr int kEpaV = 4 + kEpaIters;
+constexpr int kEpaF = 2 * kEpaV - 4;
+struct EpaScratch {
+  double V[kEpaV][3];
+  double N[kEpaF][4];      // face planes: unit outward normal, offset
+  int8_t F[kEpaF][3];
+  int8_t H[kEpaF + 4][2];  // horizon edges of one expansion
+};
+
 // Witness of the previous check of one problem (LDS): the colliding pair and,
 // when its GJK ended on an enclosing tetrahedron, the 4 search directions.
+// Continuation only: a certified penetration margin of the witness pair
+// (budget, from epa_depth_lb) and the motion bound accumulated against it
+// since (Emot = sum over updates of sum_j |dq_j| Rmot[j]); while Emot < budget
+// the pair provably still intersects, so the check's answer is known.
 template <typename T>
 struct Witness {
   int32_t pair;     // -1: none
   int32_t cert_ok;  // dir[] valid
+  int32_t skip_ok;  // budget valid for this pair
+  int32_t epa_wait; // checks before the next certificate attempt
+  int32_t gen;      // bumped whenever skip_ok / budget / Rmot change (the IK lanes cache them)
+  double budget;
+  double Emot;
+  T Rmot[kMaxNq];   // per joint: lever-arm bound of the two geometries about it
+  T gbrad[2];
+  EpaScratch epa;
   T dir[12];
   T pts[4][3];
   // the pair's two geometries, cached when the witness is set (continuation)
@@ -267,6 +291,120 @@ IKG_HD inline bool tetra_encloses_origin(const T* P0, const T* P1, const T* P2, 
   if (V == T(0)) return false;
   return vol(O, P1, P2, P3) * V > T(0) && vol(P0, O, P2, P3) * V > T(0) && vol(P0, P1, O, P3) * V > T(0) &&
          vol(P0, P1, P2, O) * V > T(0);
+}
+
+// Certified lower bound on the penetration depth of two intersecting convex
+// shapes: the expanding polytope algorithm (EPA) started from an
+// origin-enclosing tetrahedron P of support points of A - B.  Every vertex is
+// a support point, so the polytope lies inside A - B; with the origin inside
+// it, the ball of radius min over faces of the plane distance lies inside
+// A - B too, i.e. translating either shape by less than that keeps them
+// intersecting (for any rigid motion: every point moving by less than the
+// bound keeps h_{A-B}(u) > 0 for all u).  A few expansions along the closest
+// face's normal approach the true depth fast (round-1 probe on the
+// colliding fixtures: ~90% after 4).  Returns 0 when no certificate results
+// (degenerate or non-convex numerics: the final polytope is verified).
+template <typename T>
+IKG_HD inline double epa_depth_lb(const Shape<T>& A, const Shape<T>& B, const T (*P)[3], EpaScratch& s) {
+  for (int v = 0; v < 4; ++v)
+    for (int i = 0; i < 3; ++i) s.V[v][i] = (double)P[v][i];
+  int nV = 4, nF = 4;
+  // plane of face f into s.N[f]; false if degenerate
+  auto plane = [&](int f) {
+    const double *a = s.V[s.F[f][0]], *b = s.V[s.F[f][1]], *c = s.V[s.F[f][2]];
+    const double u[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, w[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+    double n[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
+    const double nn = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    if (!(nn > 1e-300)) return false;
+    const double r = 1.0 / nn;
+    for (int i = 0; i < 3; ++i) s.N[f][i] = n[i] * r;
+    s.N[f][3] = s.N[f][0] * a[0] + s.N[f][1] * a[1] + s.N[f][2] * a[2];
+    return true;
+  };
+  const int8_t F0[4][3] = {{0, 1, 2}, {0, 3, 1}, {0, 2, 3}, {1, 3, 2}};
+  double cen[3];
+  for (int i = 0; i < 3; ++i) cen[i] = 0.25 * (s.V[0][i] + s.V[1][i] + s.V[2][i] + s.V[3][i]);
+  for (int f = 0; f < 4; ++f) {
+    for (int k = 0; k < 3; ++k) s.F[f][k] = F0[f][k];
+    if (!plane(f)) return 0.0;
+    if (s.N[f][0] * cen[0] + s.N[f][1] * cen[1] + s.N[f][2] * cen[2] > s.N[f][3]) {  // inward: flip
+      const int8_t t = s.F[f][1];
+      s.F[f][1] = s.F[f][2];
+      s.F[f][2] = t;
+      for (int i = 0; i < 4; ++i) s.N[f][i] = -s.N[f][i];
+    }
+  }
+  double best = 0.0, scale = 0.0;
+  for (int v = 0; v < 4; ++v)
+    for (int i = 0; i < 3; ++i) scale = fmax(scale, fabs(s.V[v][i]));
+  for (int it = 0;; ++it) {
+    int fmin = 0;
+    for (int f = 1; f < nF; ++f)
+      if (s.N[f][3] < s.N[fmin][3]) fmin = f;
+    const double dmin = s.N[fmin][3];
+    if (!(dmin >= 0.0)) return 0.0;  // the origin is not inside
+    best = dmin;
+    if (it == kEpaIters || nV == kEpaV) break;
+    T dir[3] = {(T)s.N[fmin][0], (T)s.N[fmin][1], (T)s.N[fmin][2]}, wt[3];
+    mink_support(A, B, dir, wt);
+    const double w[3] = {(double)wt[0], (double)wt[1], (double)wt[2]};
+    if (w[0] * s.N[fmin][0] + w[1] * s.N[fmin][1] + w[2] * s.N[fmin][2] - dmin <= 1e-12 * scale) break;
+    bool vis[kEpaF];
+    int nvis = 0;
+    for (int f = 0; f < nF; ++f) {
+      vis[f] = s.N[f][0] * w[0] + s.N[f][1] * w[1] + s.N[f][2] * w[2] - s.N[f][3] > 1e-14 * scale;
+      nvis += vis[f];
+    }
+    if (!vis[fmin]) break;
+    int nH = 0;
+    bool overflow = false;
+    for (int f = 0; f < nF && !overflow; ++f) {
+      if (!vis[f]) continue;
+      for (int e = 0; e < 3; ++e) {
+        const int8_t a = s.F[f][e], b = s.F[f][(e + 1) % 3];
+        bool shared = false;
+        for (int g = 0; g < nF && !shared; ++g) {
+          if (g == f || !vis[g]) continue;
+          for (int e2 = 0; e2 < 3; ++e2)
+            if (s.F[g][e2] == b && s.F[g][(e2 + 1) % 3] == a) shared = true;
+        }
+        if (!shared) {
+          if (nH == kEpaF + 4) {
+            overflow = true;
+            break;
+          }
+          s.H[nH][0] = a;
+          s.H[nH][1] = b;
+          ++nH;
+        }
+      }
+    }
+    if (overflow || nF - nvis + nH > kEpaF) break;  // the current polytope stays valid
+    int k = 0;
+    for (int f = 0; f < nF; ++f) {  // drop the visible faces
+      if (vis[f]) continue;
+      for (int e = 0; e < 3; ++e) s.F[k][e] = s.F[f][e];
+      for (int i = 0; i < 4; ++i) s.N[k][i] = s.N[f][i];
+      ++k;
+    }
+    for (int i = 0; i < 3; ++i) s.V[nV][i] = w[i];
+    for (int h = 0; h < nH; ++h) {
+      s.F[k][0] = s.H[h][0];
+      s.F[k][1] = s.H[h][1];
+      s.F[k][2] = (int8_t)nV;
+      if (!plane(k)) return 0.0;
+      ++k;
+    }
+    nF = k;
+    ++nV;
+    for (int i = 0; i < 3; ++i) scale = fmax(scale, fabs(w[i]));
+  }
+  // verify: every vertex on the inner side of every face plane (convex hull)
+  for (int f = 0; f < nF; ++f)
+    for (int v = 0; v < nV; ++v)
+      if (s.N[f][0] * s.V[v][0] + s.N[f][1] * s.V[v][1] + s.N[f][2] * s.V[v][2] - s.N[f][3] > 1e-9 * scale)
+        return 0.0;
+  return best;
 }
 
 // Narrow phase of one pair (hpp-fcl collide(): intersection <=> collision).

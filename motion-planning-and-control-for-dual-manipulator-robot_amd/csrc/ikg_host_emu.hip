@@ -175,3 +175,23 @@ extern "C" int ikg_emu_collision(const ikg_model_desc* d, const ikg_collision_de
     emu_col<float>(d, cd, q, targets, B, out);
   return 0;
 }
+
+// EPA depth certificate of one shape pair (tests/test_collision_epa.py):
+// kinds/placements/dims per ikg_collision_desc conventions; returns
+// pair_collides' verdict in *r and the certified depth bound in *depth (0 when
+// no certificate).
+extern "C" int ikg_emu_epa(int kindA, const double* RA, const double* tA, const double* dA, int kindB,
+                           const double* RB, const double* tB, const double* dB, int* r, double* depth) {
+  using namespace ikg;
+  const Shape<double> A{RA, tA, dA, kindA}, B{RB, tB, dB, kindB};
+  double cert[12];
+  *r = pair_collides(A, B, cert);
+  *depth = 0.0;
+  if (*r != 2) return 0;
+  double pts[4][3];
+  for (int k = 0; k < 4; ++k) mink_support(A, B, cert + 3 * k, pts[k]);
+  if (!tetra_encloses_origin(pts[0], pts[1], pts[2], pts[3])) return 0;
+  EpaScratch s;
+  *depth = epa_depth_lb(A, B, pts, s);
+  return 0;
+}

@@ -25,6 +25,8 @@ dtype = sys.argv[2] if len(sys.argv) > 2 else "f64"
 s = IKSolver(device=0, scene=load_nextage_scene())
 lib = _lib.load()
 lib.ikg_debug_cprof.argtypes = [C.c_void_p, C.c_int]
+lib.ikg_debug_skip.argtypes = [C.c_void_p, C.c_int]
+sk = np.zeros(6, np.uint64)
 tdt = torch.float64 if dtype == "f64" else torch.float32
 dev = torch.device("cuda", 0)
 tg = torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device=dev)
@@ -32,12 +34,16 @@ sol = s.solve(tg, torch.zeros(15, dtype=tdt), check_collision=True)
 torch.cuda.synchronize()
 buf = np.zeros(8, np.uint64)
 lib.ikg_debug_cprof(buf.ctypes.data, 1)
+lib.ikg_debug_skip(sk.ctypes.data, 1)
 sol = s.solve(tg, torch.zeros(15, dtype=tdt), check_collision=True)
 torch.cuda.synchronize()
 lib.ikg_debug_cprof(buf.ctypes.data, 1)
+lib.ikg_debug_skip(sk.ctypes.data, 1)
 n_it = max(int(buf[7]), 1)
 names = ["fk_err", "collide", "update", "frames", "witness", "sweep", "n_sweeps", "iters"]
 out = {k: int(v) for k, v in zip(names, buf)}
 out["cycles_per_iter"] = {k: round(int(buf[i]) / n_it, 1) for i, k in enumerate(names[:6])}
 out["success"] = int(sol.converged.sum().item())
+out["certificate"] = {k: int(v) for k, v in zip(["checks_run", "checks_known", "hit_with_tetra", "epa_runs",
+                                                   "epa_certified", "margin_sum_nm"], sk)}
 print(json.dumps(out))
