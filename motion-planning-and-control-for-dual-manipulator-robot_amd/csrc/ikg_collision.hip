@@ -30,6 +30,10 @@ __device__ unsigned long long g_cprof[8];
 // certified margins (nm)
 __device__ unsigned long long g_skip[6];
 #define SKIP_STAT(i, v) atomicAdd(&g_skip[i], (unsigned long long)(v))
+// single-lane witness work: cycles in GJK (pair_collides + supports), in
+// certify_witness (of which EPA), calls of each
+__device__ unsigned long long g_wprof[6];
+#define WPROF(i, v) atomicAdd(&g_wprof[i], (unsigned long long)(v))
 // `cp_lead` (in scope at every use): this lane accumulates for its problem
 #define CPROF_MARK(acc, t)                   \
   do {                                       \
@@ -44,6 +48,9 @@ __device__ unsigned long long g_skip[6];
 #else
 #define SKIP_STAT(i, v) \
   do {                  \
+  } while (0)
+#define WPROF(i, v) \
+  do {              \
   } while (0)
 #define CPROF_MARK(acc, t) \
   do {                     \
@@ -315,38 +322,195 @@ __device__ inline GroupLds<T> group_view(char* base, int g, int nq, int ng) {
   return v;
 }
 
-// Penetration certificate of the witness pair (one lane; rare, so kept out of
-// line: inlined, its temporaries raised the register pressure of the whole
-// continuation loop).  EPA lower bound on the depth minus the placement
-// rounding of the I/O type; per joint j, the lever-arm bound Rmot[j] of the two
-// geometries about it (distance of the geometry's centre from the joint origin
-// + its bounding radius + twice the margin, which bounds that distance over the
-// motions the margin allows).
-template <typename T>
-__device__ __attribute__((noinline)) void certify_witness(int nq, Shape<T> A, Shape<T> B, Witness<T>& W,
-                                                          const T (*Fa)[12], const int32_t* par) {
-  const double tol = sizeof(T) == 8 ? 1e-9 : 1e-5;
-  const double d = epa_depth_lb(A, B, W.pts, W.epa) - tol;
-  SKIP_STAT(3, 1);
-  if (!(d > 0.0)) {
-    W.epa_wait = 32;
-    return;
-  }
-  SKIP_STAT(4, 1);
-  SKIP_STAT(5, d * 1e9);
-  for (int j = 0; j < nq; ++j) W.Rmot[j] = T(0);
-  for (int g = 0; g < 2; ++g) {
-    if (W.gtarget[g]) continue;
-    const T* c = W.P[g] + 9;
-    for (int j = W.gjoint[g]; j >= 0; j = par[j]) {
-      const T dx = c[0] - Fa[j][9], dy = c[1] - Fa[j][10], dz = c[2] - Fa[j][11];
-      W.Rmot[j] += sqrt(dx * dx + dy * dy + dz * dz) + W.gbrad[g] + T(2.0 * d);
+// ---- group-parallel EPA (continuation): the LG lanes of one problem's group
+// each own one face slot of the polytope (LG >= kEpaF); vertices and the new
+// faces of an expansion pass through LDS.  Same polytope sequence as the
+// serial epa_depth_lb (the reference form, host-tested): the closest face is
+// the lowest slot at the minimum offset, the horizon is the set of edges of
+// visible faces whose reverse edge lies on no visible face, and every face's
+// plane is computed by the same expression -- only slot order differs.
+template <int LG>
+__device__ __forceinline__ unsigned long long group_bits(bool p, int lane0) {
+  const unsigned long long b = __ballot(p);
+  return LG == 64 ? b : (b >> lane0) & ((1ull << LG) - 1ull);
+}
+
+template <int LG>
+__device__ __forceinline__ double group_min(double x) {
+#pragma unroll
+  for (int o = LG / 2; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o, LG));
+  return x;
+}
+
+// LDS writes of one lane visible to the other lanes of its wave (one wave
+// per workgroup here; the groups of a wave run the same code in lockstep)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// plane of face (a, b, c) of V: unit normal + offset; false if degenerate
+__device__ __forceinline__ bool epa_plane(const double (*V)[3], int a, int b, int c, double* n) {
+  const double *pa = V[a], *pb = V[b], *pc = V[c];
+  const double u[3] = {pb[0] - pa[0], pb[1] - pa[1], pb[2] - pa[2]};
+  const double w[3] = {pc[0] - pa[0], pc[1] - pa[1], pc[2] - pa[2]};
+  const double m[3] = {u[1] * w[2] - u[2] * w[1], u[2] * w[0] - u[0] * w[2], u[0] * w[1] - u[1] * w[0]};
+  const double nn = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+  if (!(nn > 1e-300)) return false;
+  const double r = 1.0 / nn;
+  for (int i = 0; i < 3; ++i) n[i] = m[i] * r;
+  n[3] = n[0] * pa[0] + n[1] * pa[1] + n[2] * pa[2];
+  return true;
+}
+
+template <typename T, int LG>
+__device__ double epa_depth_lb_group(const Shape<T>& A, const Shape<T>& B, const T (*P)[3], EpaScratch& s, int li,
+                                     int lane0) {
+  static_assert(LG >= kEpaF, "one face slot per lane");
+  if (li < 4)
+    for (int i = 0; i < 3; ++i) s.V[li][i] = (double)P[li][i];
+  wave_lds_sync();
+  constexpr int8_t F0[4][3] = {{0, 1, 2}, {0, 3, 1}, {0, 2, 3}, {1, 3, 2}};
+  int fa = 0, fb = 0, fc = 0;
+  double n[4] = {0.0, 0.0, 0.0, 0.0};
+  bool alive = li < 4, bad = false;
+  double cen[3], scale = 0.0;
+  for (int i = 0; i < 3; ++i) cen[i] = 0.25 * (s.V[0][i] + s.V[1][i] + s.V[2][i] + s.V[3][i]);
+  for (int v = 0; v < 4; ++v)
+    for (int i = 0; i < 3; ++i) scale = fmax(scale, fabs(s.V[v][i]));
+  if (alive) {
+    fa = F0[li][0];
+    fb = F0[li][1];
+    fc = F0[li][2];
+    bad = !epa_plane(s.V, fa, fb, fc, n);
+    if (!bad && n[0] * cen[0] + n[1] * cen[1] + n[2] * cen[2] > n[3]) {  // inward: flip
+      const int t = fb;
+      fb = fc;
+      fc = t;
+      for (int i = 0; i < 4; ++i) n[i] = -n[i];
     }
   }
-  W.budget = d;
-  W.Emot = 0.0;
-  W.skip_ok = 1;
-  ++W.gen;
+  if (group_bits<LG>(bad, lane0)) return 0.0;
+  int nV = 4;
+  double best = 0.0;
+  const unsigned long long below = li == 0 ? 0ull : (~0ull >> (64 - li));  // lanes < li of the group
+  for (int it = 0;; ++it) {
+    const double dmin = group_min<LG>(alive ? n[3] : 1e300);
+    if (!(dmin >= 0.0)) return 0.0;  // the origin is not inside
+    best = dmin;
+    if (it == kEpaIters || nV == kEpaV) break;
+    const int fmin = __ffsll((long long)group_bits<LG>(alive && n[3] == dmin, lane0)) - 1;
+    double nd[3];
+    for (int i = 0; i < 3; ++i) nd[i] = __shfl(n[i], fmin, LG);
+    T dir[3] = {(T)nd[0], (T)nd[1], (T)nd[2]}, wt[3];
+    mink_support(A, B, dir, wt);
+    const double w[3] = {(double)wt[0], (double)wt[1], (double)wt[2]};
+    if (w[0] * nd[0] + w[1] * nd[1] + w[2] * nd[2] - dmin <= 1e-12 * scale) break;
+    const bool vis = alive && n[0] * w[0] + n[1] * w[1] + n[2] * w[2] - n[3] > 1e-14 * scale;
+    const unsigned long long vm = group_bits<LG>(vis, lane0);
+    if (!((vm >> fmin) & 1ull)) break;
+    // horizon edges of this face: reverse edge on no other visible face
+    const int e0[3] = {fa, fb, fc}, e1[3] = {fb, fc, fa};
+    bool hz[3] = {vis, vis, vis};
+    for (unsigned long long m = vm; m; m &= m - 1) {
+      const int g = __ffsll((long long)m) - 1;
+      const int ga = __shfl(fa, g, LG), gb = __shfl(fb, g, LG), gc = __shfl(fc, g, LG);
+      if (g != li)
+        for (int e = 0; e < 3; ++e)
+          if ((ga == e1[e] && gb == e0[e]) || (gb == e1[e] && gc == e0[e]) || (gc == e1[e] && ga == e0[e]))
+            hz[e] = false;
+    }
+    const int nh = (int)hz[0] + (int)hz[1] + (int)hz[2];
+    const unsigned long long h1 = group_bits<LG>(nh >= 1, lane0), h2 = group_bits<LG>(nh >= 2, lane0),
+                             h3 = group_bits<LG>(nh >= 3, lane0);
+    const int nH = __popcll(h1) + __popcll(h2) + __popcll(h3);
+    const int nalive = __popcll(group_bits<LG>(alive, lane0));
+    if (nH > kEpaF + 4 || nalive - __popcll(vm) + nH > kEpaF) break;  // the current polytope stays valid
+    const int pre = __popcll(h1 & below) + __popcll(h2 & below) + __popcll(h3 & below);
+    for (int e = 0, k = pre; e < 3; ++e)
+      if (hz[e]) {
+        s.Fx[k][0] = (int8_t)e0[e];
+        s.Fx[k][1] = (int8_t)e1[e];
+        ++k;
+      }
+    if (li == 0)
+      for (int i = 0; i < 3; ++i) s.V[nV][i] = w[i];
+    wave_lds_sync();
+    // free slots: dead or visible; the r-th free slot takes the r-th new face
+    alive = alive && !vis;
+    const unsigned long long fm = group_bits<LG>(!alive, lane0);
+    const int r = __popcll(fm & below);
+    bad = false;
+    if (!alive && r < nH) {
+      fa = s.Fx[r][0];
+      fb = s.Fx[r][1];
+      fc = nV;
+      alive = true;
+      bad = !epa_plane(s.V, fa, fb, fc, n);
+    }
+    if (group_bits<LG>(bad, lane0)) return 0.0;
+    ++nV;
+    for (int i = 0; i < 3; ++i) scale = fmax(scale, fabs(w[i]));
+    wave_lds_sync();  // Fx is rewritten by the next expansion
+  }
+  // verify: every vertex on the inner side of every face plane (convex hull)
+  bool out = false;
+  if (alive)
+    for (int v = 0; v < nV; ++v)
+      out = out || n[0] * s.V[v][0] + n[1] * s.V[v][1] + n[2] * s.V[v][2] - n[3] > 1e-9 * scale;
+  return group_bits<LG>(out, lane0) ? 0.0 : best;
+}
+
+// Penetration certificate of the witness pair, by the problem's group (rare,
+// so kept out of line: inlined, its temporaries raised the register pressure
+// of the whole continuation loop).  EPA lower bound on the depth minus the
+// placement rounding of the I/O type; per joint j, the lever-arm bound Rmot[j]
+// of the two geometries about it (distance of the geometry's centre from the
+// joint origin + its bounding radius + twice the margin, which bounds that
+// distance over the motions the margin allows).
+template <typename T, int LG>
+__device__ __attribute__((noinline)) void certify_witness(int nq, Shape<T> A, Shape<T> B, Witness<T>& W,
+                                                          const T (*Fa)[12], const int32_t* par, int li, int lane0) {
+  const double tol = sizeof(T) == 8 ? 1e-9 : 1e-5;
+#ifdef IKG_CPROF
+  const unsigned long long t0 = clock64();
+#endif
+  const double d = epa_depth_lb_group<T, LG>(A, B, W.pts, W.epa, li, lane0) - tol;
+#ifdef IKG_CPROF
+  if (li == 0) {
+    WPROF(2, clock64() - t0);
+    WPROF(5, 1);
+  }
+#endif
+  if (li == 0) SKIP_STAT(3, 1);
+  if (!(d > 0.0)) {
+    if (li == 0) W.epa_wait = 32;
+    return;
+  }
+  if (li == 0) {
+    SKIP_STAT(4, 1);
+    SKIP_STAT(5, d * 1e9);
+  }
+  for (int j = li; j < nq; j += LG) {
+    T r = T(0);
+    for (int g = 0; g < 2; ++g) {
+      if (W.gtarget[g]) continue;
+      bool anc = false;
+      for (int k = W.gjoint[g]; k >= 0 && !anc; k = par[k]) anc = k == j;
+      if (!anc) continue;
+      const T* c = W.P[g] + 9;
+      const T dx = c[0] - Fa[j][9], dy = c[1] - Fa[j][10], dz = c[2] - Fa[j][11];
+      r += sqrt(dx * dx + dy * dy + dz * dz) + W.gbrad[g] + T(2.0 * d);
+    }
+    W.Rmot[j] = r;
+  }
+  if (li == 0) {
+    W.budget = d;
+    W.Emot = 0.0;
+    W.skip_ok = 1;
+    ++W.gen;
+  }
 }
 
 // One collision check for every group with `need` set (group-uniform); all 64
@@ -415,7 +579,14 @@ __device__ bool collide_group(const KModel<T>* __restrict__ m, const KCollision<
       tetra = true;
     } else {
       T cd[12];
+#ifdef IKG_CPROF
+      const unsigned long long t0 = clock64();
+#endif
       r = pair_collides(A, B, cd);
+#ifdef IKG_CPROF
+      WPROF(0, clock64() - t0);
+      WPROF(3, 1);
+#endif
       W.cert_ok = r == 2;
       if (r == 2) {
         for (int i = 0; i < 12; ++i) W.dir[i] = cd[i];
@@ -427,7 +598,20 @@ __device__ bool collide_group(const KModel<T>* __restrict__ m, const KCollision<
     if (r && tetra) SKIP_STAT(2, 1);
     // penetration certificate: while the accumulated motion bound stays below
     // it, later checks of this problem are answered without running them
-    if (r && tetra && !W.skip_ok && --W.epa_wait <= 0) certify_witness<T>(m->nq, A, B, W, Fa, V.par);
+    W.epa_go = r && tetra && !W.skip_ok && --W.epa_wait <= 0;
+  }
+  __syncthreads();
+  if (has_w && W.epa_go) {
+#ifdef IKG_CPROF
+    const unsigned long long t0 = clock64();
+#endif
+    certify_witness<T, LG>(m->nq, A, B, W, Fa, V.par, li, lane0);
+#ifdef IKG_CPROF
+    if (li == 0) {
+      WPROF(1, clock64() - t0);
+      WPROF(4, 1);
+    }
+#endif
   }
   __syncthreads();
   bool hit = has_w && V.flag[1] != T(0);
@@ -479,11 +663,20 @@ __device__ bool collide_group(const KModel<T>* __restrict__ m, const KCollision<
 // One continuation iteration's FK + errors + step of this lane's arm
 // (inverse_geometry.py:58-83; the IK lanes' frames go to F for the check).
 // Returns the squared error norm of the lane's hand.
-template <typename T, bool DAMPED, class SP>
+// FRAMES = false (certified stretches, no check ahead): the batch kernel's
+// chest-frame FK with the tracked rotation angle, no joint frames.
+template <typename T, bool DAMPED, class SP, bool FRAMES = true>
 __device__ __forceinline__ T cont_step(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, const T* sn,
-                                       const T* cs, const T* RT, const T* tT, T (*F)[12], T* dq, T& s) {
+                                       const T* cs, const T* RT, const T* tT, T (*F)[12], T* dq, T& s,
+                                       ThetaTrack<T>* tk = nullptr, bool resync = true) {
   ArmState<T> st;
-  const T x = arm_fk_error<T, SP, true>(m, arm, sn, cs, RT, tT, st, F);
+  T x;
+  if constexpr (FRAMES)
+    x = arm_fk_error<T, SP, true>(m, arm, sn, cs, RT, tT, st, F);
+  else if constexpr (IKG_THETA_TRACK && is_f64<T>)
+    x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, tk, resync);
+  else
+    x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
   T alpha, beta;
   if constexpr (!DAMPED) {
     T u[6], v[6];
@@ -500,22 +693,31 @@ __device__ __forceinline__ T cont_step(const KModel<T>* __restrict__ m, const KP
   return x;
 }
 
-// q <- clip(q + dt dq) (:86-89), the certificate's motion bound
-// sum_j |dq_j| Rmot[j] over the root and the lane's arm joints, the trig state.
+// Certificate motion bound of this lane's joints between the certified
+// iterate and q: sum_j |q_j - qcert_j| Rmot_j.  Moving one joint at a time
+// from qcert to q, every point of the witness geometries moves by at most
+// Rmot_j |dq_j| per joint while the total stays below the margin (Rmot holds
+// the 2 x margin lever-arm allowance), so the net displacement bounds any
+// iterate -- tighter than summing the per-update motion when iterates drift
+// back and forth near a fixed point.
+template <typename T>
+__device__ __forceinline__ T motion_bound(T qc, const T* qa, const T* qcert, const T* Rr) {
+  T e = fabs(qc - qcert[0]) * Rr[0];
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) e += fabs(qa[k] - qcert[k + 1]) * Rr[k + 1];
+  return e;
+}
+
+// q <- clip(q + dt dq) (:86-89) and the trig state.
 template <typename T>
 __device__ __forceinline__ void cont_update(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, T s,
-                                            const T* dq, int it, bool cert_live, const T* Rr, T& emot, T& qc, T* qa,
+                                            const T* dq, int it, T& qc, T* qa,
                                             T* sn, T* cs) {
   T q_old[7];
   q_old[0] = qc;
 #pragma unroll
   for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
   arm_update(m, arm, prm.dt, s, dq, qc, qa);
-  if (cert_live) {
-    emot += fabs(qc - q_old[0]) * Rr[0];
-#pragma unroll
-    for (int k = 0; k < kArmDof; ++k) emot += fabs(qa[k] - q_old[k + 1]) * Rr[k + 1];
-  }
   trig_advance(qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);
 }
 
@@ -528,7 +730,10 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
                                                                   uint8_t* __restrict__ conv,
                                                                   int32_t* __restrict__ iters,
                                                                   T* __restrict__ err,
-                                                                  const int32_t* __restrict__ witness) {
+                                                                  int32_t* __restrict__ witness, int handoff,
+                                                                  int32_t* __restrict__ stretch_list,
+                                                                  int32_t* __restrict__ stretch_count,
+                                                                  T* __restrict__ stretch_rec) {
   extern __shared__ __align__(16) char lds[];
   constexpr int LG = 64 / G;
   const int lane = threadIdx.x;
@@ -572,6 +777,7 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
       V.W->gen = 0;
       V.W->budget = 0.0;
       V.W->Emot = 0.0;
+      V.flag[3] = T(0);
     }
   }
   __syncthreads();
@@ -598,33 +804,58 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
   // budget / Rmot of their chain joints) and the motion bound accumulated
   // against it, in registers: no LDS traffic per iteration but one int read
   int cgen = 0;
-  bool cert_live = false;
+  bool cert_live = false, handed = false;
   T Rr[7] = {};
-  T emot = T(0), cbudget = T(0);
+  T qcert[7] = {}, cbudget = T(0);
   for (;;) {
 #ifdef IKG_CPROF
     cp_lead = li == 0 && active;
 #endif
     // Certified stretch: while the witness pair provably intersects, the
-    // reference's stop test cannot pass, so the IK lanes iterate alone at the
-    // batch kernel's pace (no LDS flags, no barriers).  They leave at the
-    // first iterate whose errors pass once the margin is spent (the loop below
-    // redoes that iterate and runs a real check) or at max_iters.
+    // reference's stop test cannot pass, so the IK lanes iterate alone (no
+    // LDS flags, no barriers, no joint frames).  handoff != 0: the problem
+    // leaves for ikg_cert_stretch_kernel (pair layout, the batch kernel's
+    // registers and pace) with its remaining margin; otherwise the stretch
+    // runs here.  Either way it ends at the first iterate whose errors pass
+    // once the margin is spent (redone below with a real check) or at max_iters.
     if (active && li < 2 && cert_live && passive_clamped) {
-      for (;;) {
-        if (it >= prm.max_iters) break;
-        T dq[6], s;
-        const T x = cont_step<T, DAMPED, SP>(m, prm, arm, sn, cs, RT, tT, V.F, dq, s);
-        const T xo = pair_swap(x);
-        if (x < prm.eps2 && xo < prm.eps2) {
-          if (!(emot + pair_swap(emot) < cbudget)) break;
-          if (li == 0) SKIP_STAT(1, 1);
+      if (handoff) {
+        if (li == 0) {
+          V.flag[3] = T(1);
+          stretch_rec[p * kStretchRec] = cbudget;
         }
-        cont_update(m, prm, arm, s, dq, it, cert_live, Rr, emot, qc, qa, sn, cs);
-        ++it;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          stretch_rec[p * kStretchRec + 1 + 7 * arm + k] = Rr[k];
+          stretch_rec[p * kStretchRec + 15 + 7 * arm + k] = qcert[k];
+        }
+      } else {
+        ThetaTrack<T> tk{};
+        for (int n = 0;; ++n) {
+          if (it >= prm.max_iters) break;
+          T dq[6], s;
+          const T x = cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, &tk,
+                                                      n == 0 || (it % Trig<T>::kResync) == 0);
+          const T xo = pair_swap(x);
+          const T em = motion_bound(qc, qa, qcert, Rr);
+          const T et = em + pair_swap(em);
+          if (x < prm.eps2 && xo < prm.eps2) {
+            if (!(et < cbudget)) break;
+            if (li == 0) SKIP_STAT(1, 1);
+          }
+          cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
+          ++it;
+        }
+        if (arm == 0) V.q[m->root_q] = qc;
+        for (int k = 0; k < kArmDof; ++k) V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
       }
-      if (arm == 0) V.q[m->root_q] = qc;
-      for (int k = 0; k < kArmDof; ++k) V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
+    }
+    if (handoff) {
+      __syncthreads();
+      if (active && V.flag[3] != T(0)) {
+        handed = true;
+        active = false;
+      }
     }
     __syncthreads();
     // FK + errors at the current iterate (:58-67) and, before the collision
@@ -640,7 +871,8 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
         cert_live = false;
       }
       // collision(q) is known True while the motion bound stays below the margin
-      const T tot = emot + pair_swap(emot);
+      const T em = cert_live ? motion_bound(qc, qa, qcert, Rr) : T(0);
+      const T tot = em + pair_swap(em);
       if (li == 0) V.flag[2] = (cert_live && tot < cbudget) ? T(1) : T(0);
     }
     __syncthreads();
@@ -672,7 +904,9 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
       // bound counts the motion from this iterate on
       cgen = V.W->gen;
       cert_live = V.W->skip_ok != 0;
-      emot = T(0);
+      qcert[0] = qc;
+#pragma unroll
+      for (int k = 0; k < kArmDof; ++k) qcert[k + 1] = qa[k];
       if (cert_live) {
         cbudget = T(V.W->budget);
         Rr[0] = arm == 0 ? V.W->Rmot[m->root_q] : T(0);  // the root is counted once (left lane)
@@ -680,7 +914,7 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
       }
     }
     if (active && li < 2) {  // apply the update (:86-89)
-      cont_update(m, prm, arm, s, dq, it, cert_live, Rr, emot, qc, qa, sn, cs);
+      cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
       if (arm == 0) V.q[m->root_q] = qc;
       for (int k = 0; k < kArmDof; ++k) V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
     }
@@ -719,10 +953,94 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
 #endif
   if (started) {
     for (int j = li; j < nq; j += LG) q_out[p * nq + j] = V.q[j];
-    if (li < 2) err[p * 2 + arm] = sqrt(nrm);
-    if (li == 0) {
-      conv[p] = success ? 1 : 0;
+    if (handed) {  // continues in ikg_cert_stretch_kernel: pending (-2 - pair), listed
+      if (li == 0) {
+        iters[p] = it;
+        witness[p] = -2 - V.W->pair;
+        stretch_list[atomicAdd(stretch_count, 1)] = (int32_t)p;
+      }
+    } else {
+      if (li < 2) err[p * 2 + arm] = sqrt(nrm);
+      if (li == 0) {
+        conv[p] = success ? 1 : 0;
+        iters[p] = it;
+        witness[p] = -1;  // final
+      }
+    }
+  }
+}
+
+// Certified stretches handed off by the continuation (stretch_list): pair
+// layout as in ikg_pair_batch_kernel (two lanes per problem, up to 32 per
+// wave, spread over the chip when few), the batch kernel's chest-frame
+// iteration, with the continuation's margin test: while the motion bound
+// stays below the remaining certified margin the witness pair still
+// intersects, so the stop test of inverse_geometry.py:70 cannot pass.  Ends
+// at max_iters (final: not converged) or at the first iterate whose errors
+// pass once the margin is spent (witness[p] back to the pair: the next
+// continuation launch redoes that iterate with a real check).
+template <typename T, bool DAMPED, class SP>
+__global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
+                                                              const T* __restrict__ targets, int64_t S_per_target,
+                                                              T* __restrict__ q_out, uint8_t* __restrict__ conv,
+                                                              int32_t* __restrict__ iters, T* __restrict__ err,
+                                                              int32_t* __restrict__ witness,
+                                                              const int32_t* __restrict__ stretch_list,
+                                                              const int32_t* __restrict__ stretch_count,
+                                                              const T* __restrict__ stretch_rec, int ppw_min) {
+  const int n = *stretch_count;
+  const int lane = threadIdx.x, arm = lane & 1;
+  const int nb = (int)gridDim.x;
+  const int ppw = min(32, max(ppw_min, (n + nb - 1) / nb));
+  const int nq = m->nq;
+  for (int base = (int)blockIdx.x * ppw; base < n; base += nb * ppw) {
+    const int i = base + (lane >> 1);
+    if (lane >= 2 * ppw || i >= n) continue;  // both lanes of a pair together
+    const int64_t p = stretch_list[i];
+    const int64_t tgt = S_per_target > 1 ? p / S_per_target : p;
+    T RT[9], tT[3], qc, qa[kArmDof], sn[7], cs[7], Rr[7], qcert[7];
+    hook_target(m, arm, targets + tgt * 12, RT, tT);
+    T* qrow = q_out + p * nq;
+    qc = qrow[m->root_q];
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) qa[k] = qrow[arm ? m->arm_q[1][k] : m->arm_q[0][k]];
+    trig_exact(qc, qa, sn, cs);
+    const T budget = stretch_rec[p * kStretchRec];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      Rr[k] = stretch_rec[p * kStretchRec + 1 + 7 * arm + k];
+      qcert[k] = stretch_rec[p * kStretchRec + 15 + 7 * arm + k];
+    }
+    int it = iters[p];
+    T x;
+    bool final = false;
+    ThetaTrack<T> tk{};
+    for (int r = 0;; ++r) {
+      T dq[6], s;
+      x = cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, &tk,
+                                          r == 0 || (it % Trig<T>::kResync) == 0);
+      const T xo = pair_swap(x);
+      const T em = motion_bound(qc, qa, qcert, Rr);
+      const T et = em + pair_swap(em);
+      if (it >= prm.max_iters) {  // loop exhausted (:100): the last errors are reported
+        final = true;
+        break;
+      }
+      if (x < prm.eps2 && xo < prm.eps2) {
+        if (!(et < budget)) break;
+        if (arm == 0) SKIP_STAT(1, 1);
+      }
+      cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
+      ++it;
+    }
+    if (arm == 0) qrow[m->root_q] = qc;
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) qrow[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
+    if (final) err[p * 2 + arm] = sqrt(x);
+    if (arm == 0) {
       iters[p] = it;
+      if (final) conv[p] = 0;
+      witness[p] = final ? -1 : -2 - witness[p];
     }
   }
 }
@@ -782,22 +1100,70 @@ static int cont_groups() {
   return v;
 }
 
+// stream-ordered workspace of one continuation: witness / state per problem
+// (>= 0: continue with this pair, -1: final, <= -2: stretch pending), the
+// stretch list and its count, the stretch records (remaining margin + Rmot)
+template <typename T>
+struct ContWs {
+  int32_t* wit;
+  int32_t* list;
+  int32_t* count;
+  T* rec;
+};
+
+// Continuation launches that hand certified stretches to the stretch kernel
+// before the last one, which runs any remaining stretch itself.  Every round
+// is a grid-wide sync, and a problem whose margin runs out mid-stretch waits
+// for the round's longest stretch before its re-check: with few continued
+// problems (latency-bound, a wave or less per SIMD) the in-kernel stretch is
+// faster; with many (throughput-bound) the stretch kernel's 32 problems per
+// wave win.  Measured (tools/probe/rounds.sh, kernel ms per solve):
+// C2 fp64 B=4096: 0 rounds 2.66, 2 rounds 3.10; C3 fp32 B=65536: 6.00, 5.71.
+// IKG_HANDOFF_ROUNDS overrides (read per launch: the tests run both paths).
+static int handoff_rounds(int64_t B) {
+  const char* e = getenv("IKG_HANDOFF_ROUNDS");
+  if (e) return std::min(64, std::max(0, atoi(e)));
+  return B > 16384 ? 2 : 0;
+}
+
+// least problems per stretch wave (IKG_STRETCH_PPW; timing knob)
+static int stretch_ppw() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("IKG_STRETCH_PPW");
+    v = e ? std::min(32, std::max(1, atoi(e))) : 32;
+  }
+  return v;
+}
+
 template <typename T, bool DAMPED, class SP, int G>
 static void launch_continue_g(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
-                              const BatchArgs& a, int nq, int ng, const int32_t* wit, hipStream_t s) {
+                              const BatchArgs& a, int nq, int ng, const ContWs<T>& w, hipStream_t s) {
   const size_t lds = (size_t)G * group_lds_bytes<T>(nq, ng);
-  hipLaunchKernelGGL((ikg_collide_continue_kernel<T, DAMPED, SP, G>), dim3((unsigned)((a.B + G - 1) / G)), dim3(64),
-                     lds, s, dm, dc, prm, (const T*)a.targets, a.S, a.B, (T*)a.q_out, a.converged, a.iters,
-                     (T*)a.err_out, wit);
+  const dim3 grid((unsigned)((a.B + G - 1) / G));
+  // stretch kernel: enough waves to give every SIMD of the chip one, at most
+  const unsigned sgrid = (unsigned)std::min<int64_t>(1024, a.B);
+  const int rounds = handoff_rounds(a.B);
+  for (int r = 0; r <= rounds; ++r) {
+    const int handoff = r < rounds;
+    if (handoff) (void)hipMemsetAsync(w.count, 0, sizeof(int32_t), s);
+    hipLaunchKernelGGL((ikg_collide_continue_kernel<T, DAMPED, SP, G>), grid, dim3(64), lds, s, dm, dc, prm,
+                       (const T*)a.targets, a.S, a.B, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, w.wit,
+                       handoff, w.list, w.count, w.rec);
+    if (handoff)
+      hipLaunchKernelGGL((ikg_cert_stretch_kernel<T, DAMPED, SP>), dim3(sgrid), dim3(64), 0, s, dm, prm,
+                         (const T*)a.targets, a.S, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, w.wit,
+                         (const int32_t*)w.list, (const int32_t*)w.count, (const T*)w.rec, stretch_ppw());
+  }
 }
 
 template <typename T, bool DAMPED, class SP>
 static void launch_continue_t(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
-                              const BatchArgs& a, int nq, int ng, const int32_t* wit, hipStream_t s) {
+                              const BatchArgs& a, int nq, int ng, const ContWs<T>& w, hipStream_t s) {
   if (cont_groups() == 1)
-    launch_continue_g<T, DAMPED, SP, 1>(dm, dc, prm, a, nq, ng, wit, s);
+    launch_continue_g<T, DAMPED, SP, 1>(dm, dc, prm, a, nq, ng, w, s);
   else
-    launch_continue_g<T, DAMPED, SP, 4>(dm, dc, prm, a, nq, ng, wit, s);
+    launch_continue_g<T, DAMPED, SP, 4>(dm, dc, prm, a, nq, ng, w, s);
 }
 
 template <typename T>
@@ -806,25 +1172,27 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
   if (a.B <= 0) return hipSuccess;
   if (a.B > 0x7fffffff) return hipErrorInvalidValue;
   // stream-ordered workspace: the pre-screen's witness pair per problem
-  int32_t* wit = nullptr;
-  hipError_t e = hipMallocAsync((void**)&wit, sizeof(int32_t) * a.B, s);
+  const size_t ib = ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255);
+  char* ws = nullptr;
+  hipError_t e = hipMallocAsync((void**)&ws, 2 * ib + 256 + sizeof(T) * kStretchRec * (size_t)a.B, s);
   if (e != hipSuccess) return e;
+  ContWs<T> w{(int32_t*)ws, (int32_t*)(ws + ib), (int32_t*)(ws + 2 * ib), (T*)(ws + 2 * ib + 256)};
   hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
-                     (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, wit);
+                     (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
   const bool damped = prm.lambda > T(0);
   if (spec == kSpecNextage) {
     if (damped)
-      launch_continue_t<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, wit, s);
+      launch_continue_t<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, w, s);
     else
-      launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, nq, ng, wit, s);
+      launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, nq, ng, w, s);
   } else {
     if (damped)
-      launch_continue_t<T, true, SpecGeneric>(dm, dc, prm, a, nq, ng, wit, s);
+      launch_continue_t<T, true, SpecGeneric>(dm, dc, prm, a, nq, ng, w, s);
     else
-      launch_continue_t<T, false, SpecGeneric>(dm, dc, prm, a, nq, ng, wit, s);
+      launch_continue_t<T, false, SpecGeneric>(dm, dc, prm, a, nq, ng, w, s);
   }
   e = hipGetLastError();
-  const hipError_t ef = hipFreeAsync(wit, s);
+  const hipError_t ef = hipFreeAsync(ws, s);
   return e != hipSuccess ? e : ef;
 }
 
@@ -834,6 +1202,14 @@ extern "C" int ikg_debug_skip(unsigned long long* out, int reset) {
   if (reset) {
     unsigned long long z[6] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_skip), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+extern "C" int ikg_debug_wprof(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wprof), sizeof(g_wprof)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[6] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;
 }

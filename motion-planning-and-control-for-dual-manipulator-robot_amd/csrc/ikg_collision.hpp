@@ -49,13 +49,18 @@ struct CollideScratch {
 // Expanding-polytope scratch (epa_depth_lb): at most kEpaIters expansions of
 // the starting tetrahedron.
 constexpr int kEpaIters = 5;
+// continuation -> stretch kernel record per problem: the certified margin,
+// Rmot of the root + left arm joints and of (0 +) the right arm's, then the
+// certified iterate's values of the same joints per arm
+constexpr int kStretchRec = 32;
 constexpr int kEpaV = 4 + kEpaIters;
 constexpr int kEpaF = 2 * kEpaV - 4;
 struct EpaScratch {
   double V[kEpaV][3];
   double N[kEpaF][4];      // face planes: unit outward normal, offset
   int8_t F[kEpaF][3];
-  int8_t H[kEpaF + 4][2];  // horizon edges of one expansion
+  int8_t H[kEpaF + 4][2];  // horizon edges of one expansion (serial form)
+  int8_t Fx[kEpaF + 4][2]; // new faces of one expansion (group form)
 };
 
 // Witness of the previous check of one problem (LDS): the colliding pair and,
@@ -71,6 +76,7 @@ struct Witness {
   int32_t skip_ok;  // budget valid for this pair
   int32_t epa_wait; // checks before the next certificate attempt
   int32_t gen;      // bumped whenever skip_ok / budget / Rmot change (the IK lanes cache them)
+  int32_t epa_go;   // this check's hit asks for a certificate (continuation)
   double budget;
   double Emot;
   T Rmot[kMaxNq];   // per joint: lever-arm bound of the two geometries about it

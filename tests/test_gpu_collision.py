@@ -67,7 +67,15 @@ def test_collision_batch_large_is_consistent(csolver, col_cases):
     assert np.array_equal(got, base)
 
 
-def test_solve_with_collision_fp64(csolver, solve_cases, oracle_cases):
+# continuation schedule: the size-based default, certified stretches run inside
+# the continuation kernel (0 rounds), handed to ikg_cert_stretch_kernel (2)
+ROUNDS = [None, "0", "2"]
+
+
+@pytest.mark.parametrize("rounds", ROUNDS)
+def test_solve_with_collision_fp64(csolver, solve_cases, oracle_cases, rounds, monkeypatch):
+    if rounds is not None:
+        monkeypatch.setenv("IKG_HANDOFF_ROUNDS", rounds)
     c = solve_cases
     sol = csolver.solve(c["targets"], c["q0"], check_collision=True)
     assert np.array_equal(sol.converged, c["success"])
@@ -83,7 +91,10 @@ def test_solve_with_collision_fp64(csolver, solve_cases, oracle_cases):
     assert csolver.collision(sol.q[cont], c["targets"][cont]).all()
 
 
-def test_solve_with_collision_fp32(csolver, solve_cases):
+@pytest.mark.parametrize("rounds", ROUNDS)
+def test_solve_with_collision_fp32(csolver, solve_cases, rounds, monkeypatch):
+    if rounds is not None:
+        monkeypatch.setenv("IKG_HANDOFF_ROUNDS", rounds)
     c = solve_cases
     sol = csolver.solve(c["targets"], c["q0"], dtype="f32", check_collision=True)
     agree = (sol.converged == c["success"]).mean()

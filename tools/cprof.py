@@ -26,6 +26,8 @@ s = IKSolver(device=0, scene=load_nextage_scene())
 lib = _lib.load()
 lib.ikg_debug_cprof.argtypes = [C.c_void_p, C.c_int]
 lib.ikg_debug_skip.argtypes = [C.c_void_p, C.c_int]
+lib.ikg_debug_wprof.argtypes = [C.c_void_p, C.c_int]
+wp = np.zeros(6, np.uint64)
 sk = np.zeros(6, np.uint64)
 tdt = torch.float64 if dtype == "f64" else torch.float32
 dev = torch.device("cuda", 0)
@@ -35,10 +37,12 @@ torch.cuda.synchronize()
 buf = np.zeros(8, np.uint64)
 lib.ikg_debug_cprof(buf.ctypes.data, 1)
 lib.ikg_debug_skip(sk.ctypes.data, 1)
+lib.ikg_debug_wprof(wp.ctypes.data, 1)
 sol = s.solve(tg, torch.zeros(15, dtype=tdt), check_collision=True)
 torch.cuda.synchronize()
 lib.ikg_debug_cprof(buf.ctypes.data, 1)
 lib.ikg_debug_skip(sk.ctypes.data, 1)
+lib.ikg_debug_wprof(wp.ctypes.data, 1)
 n_it = max(int(buf[7]), 1)
 names = ["fk_err", "collide", "update", "frames", "witness", "sweep", "n_sweeps", "iters"]
 out = {k: int(v) for k, v in zip(names, buf)}
@@ -46,4 +50,13 @@ out["cycles_per_iter"] = {k: round(int(buf[i]) / n_it, 1) for i, k in enumerate(
 out["success"] = int(sol.converged.sum().item())
 out["certificate"] = {k: int(v) for k, v in zip(["checks_run", "checks_known", "hit_with_tetra", "epa_runs",
                                                    "epa_certified", "margin_sum_nm"], sk)}
+out["witness_lane_cycles"] = {"gjk_per_call": int(wp[0]) // max(int(wp[3]), 1), "gjk_calls": int(wp[3]),
+                               "certify_per_call": int(wp[1]) // max(int(wp[4]), 1), "certify_calls": int(wp[4]),
+                               "epa_per_call": int(wp[2]) // max(int(wp[5]), 1)}
+s0 = s.solve(tg, torch.zeros(15, dtype=tdt), check_collision=False)
+d = (sol.iters - s0.iters).cpu().numpy()
+d = d[d != 0]
+out["continued"] = {"problems": int(d.size), "max_extra_iters": int(d.max()) if d.size else 0,
+                    "mean_extra_iters": float(d.mean()) if d.size else 0.0,
+                    "p90": float(np.percentile(d, 90)) if d.size else 0.0}
 print(json.dumps(out))
