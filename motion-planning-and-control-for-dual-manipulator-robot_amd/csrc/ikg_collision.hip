@@ -830,19 +830,23 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
           stretch_rec[p * kStretchRec + 15 + 7 * arm + k] = qcert[k];
         }
       } else {
+        // The wave's problems leave together, as soon as one of them needs the
+        // main loop (a check, or max_iters): a problem left waiting while the
+        // others finish their stretches would run its own remainder after
+        // them (measured: 4x the wave's iterations with 4 problems per wave).
+        // The others simply redo their current iterate in the main loop.
         ThetaTrack<T> tk{};
         for (int n = 0;; ++n) {
-          if (it >= prm.max_iters) break;
+          if (__any(it >= prm.max_iters)) break;
           T dq[6], s;
           const T x = cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, &tk,
                                                       n == 0 || (it % Trig<T>::kResync) == 0);
           const T xo = pair_swap(x);
           const T em = motion_bound(qc, qa, qcert, Rr);
           const T et = em + pair_swap(em);
-          if (x < prm.eps2 && xo < prm.eps2) {
-            if (!(et < cbudget)) break;
-            if (li == 0) SKIP_STAT(1, 1);
-          }
+          const bool conv2 = x < prm.eps2 && xo < prm.eps2;
+          if (__any(conv2 && !(et < cbudget))) break;
+          if (conv2 && li == 0) SKIP_STAT(1, 1);
           cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
           ++it;
         }
@@ -1117,13 +1121,13 @@ struct ContWs {
 // for the round's longest stretch before its re-check: with few continued
 // problems (latency-bound, a wave or less per SIMD) the in-kernel stretch is
 // faster; with many (throughput-bound) the stretch kernel's 32 problems per
-// wave win.  Measured (tools/probe/rounds.sh, kernel ms per solve):
-// C2 fp64 B=4096: 0 rounds 2.66, 2 rounds 3.10; C3 fp32 B=65536: 6.00, 5.71.
+// wave win.  Measured (tools/probe/rounds.sh, kernel ms per solve, 0/1/2
+// rounds): C2 fp64 B=4096: 2.47/3.45/3.17; C3 fp32 B=65536: 6.06/5.20/5.72.
 // IKG_HANDOFF_ROUNDS overrides (read per launch: the tests run both paths).
 static int handoff_rounds(int64_t B) {
   const char* e = getenv("IKG_HANDOFF_ROUNDS");
   if (e) return std::min(64, std::max(0, atoi(e)));
-  return B > 16384 ? 2 : 0;
+  return B > 16384 ? 1 : 0;
 }
 
 // least problems per stretch wave (IKG_STRETCH_PPW; timing knob)
