@@ -28,7 +28,7 @@ __device__ unsigned long long g_cprof[8];
 // certificate statistics: checks run, checks answered by the certificate,
 // tetrahedra available on a hit, EPA attempts, EPA certificates, sum of
 // certified margins (nm)
-__device__ unsigned long long g_skip[6];
+__device__ unsigned long long g_skip[8];
 #define SKIP_STAT(i, v) atomicAdd(&g_skip[i], (unsigned long long)(v))
 // single-lane witness work: cycles in GJK (pair_collides + supports), in
 // certify_witness (of which EPA), calls of each
@@ -721,6 +721,69 @@ __device__ __forceinline__ void cont_update(const KModel<T>* __restrict__ m, con
   trig_advance(qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);
 }
 
+// In-kernel certified stretch (IK lanes of the continuation).  The wave's
+// problems leave together, as soon as one of them needs the main loop (a
+// check, or max_iters): a problem left waiting while the others finish their
+// stretches would run its own remainder after them (measured: 4x the wave's
+// iterations with 4 problems per wave).  The others simply redo their current
+// iterate in the main loop.  Out of line so that the loop gets a register
+// allocation of its own: inlined into the continuation kernel, whose live
+// state spills it to AGPRs, the same iteration issued 4.5x the VALU
+// instructions of ikg_cert_stretch_kernel's (PMC).  The caller's state is
+// saved once per stretch instead.
+template <typename T, bool DAMPED, class SP>
+__device__ __noinline__ void cert_stretch(const KModel<T>* __restrict__ m, int max_iters, T eps2, T dt, T lambda,
+                                          int arm, int li, const T* RT_, const T* tT_, const T* Rr_,
+                                          const T* qcert_, T cbudget, T& qc_io, T* qa_io, T* sn_io, T* cs_io,
+                                          int& it_io) {
+  KParams<T> prm;
+  prm.max_iters = max_iters;
+  prm.eps2 = eps2;
+  prm.dt = dt;
+  prm.lambda = lambda;
+  T RT[9], tT[3], Rr[7], qcert[7], qa[kArmDof], sn[7], cs[7];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) RT[i] = RT_[i];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) tT[i] = tT_[i];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    Rr[i] = Rr_[i];
+    qcert[i] = qcert_[i];
+    sn[i] = sn_io[i];
+    cs[i] = cs_io[i];
+  }
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) qa[k] = qa_io[k];
+  T qc = qc_io;
+  int it = it_io;
+  ThetaTrack<T> tk{};
+  for (int n = 0;; ++n) {
+    if (__any(it >= max_iters)) break;
+    T dq[6], s;
+    const T x = cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, &tk,
+                                                n == 0 || (it % Trig<T>::kResync) == 0);
+    const T xo = pair_swap(x);
+    const T em = motion_bound(qc, qa, qcert, Rr);
+    const T et = em + pair_swap(em);
+    const bool conv2 = x < eps2 && xo < eps2;
+    if (__any(conv2 && !(et < cbudget))) break;
+    if (conv2 && li == 0) SKIP_STAT(1, 1);
+    if (li == 0) SKIP_STAT(6, 1);
+    cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
+    ++it;
+  }
+  qc_io = qc;
+  it_io = it;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    sn_io[i] = sn[i];
+    cs_io[i] = cs[i];
+  }
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) qa_io[k] = qa[k];
+}
+
 template <typename T, bool DAMPED, class SP, int G>
 __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T>* __restrict__ m,
                                                                   const KCollision<T>* __restrict__ c,
@@ -830,26 +893,8 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
           stretch_rec[p * kStretchRec + 15 + 7 * arm + k] = qcert[k];
         }
       } else {
-        // The wave's problems leave together, as soon as one of them needs the
-        // main loop (a check, or max_iters): a problem left waiting while the
-        // others finish their stretches would run its own remainder after
-        // them (measured: 4x the wave's iterations with 4 problems per wave).
-        // The others simply redo their current iterate in the main loop.
-        ThetaTrack<T> tk{};
-        for (int n = 0;; ++n) {
-          if (__any(it >= prm.max_iters)) break;
-          T dq[6], s;
-          const T x = cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, &tk,
-                                                      n == 0 || (it % Trig<T>::kResync) == 0);
-          const T xo = pair_swap(x);
-          const T em = motion_bound(qc, qa, qcert, Rr);
-          const T et = em + pair_swap(em);
-          const bool conv2 = x < prm.eps2 && xo < prm.eps2;
-          if (__any(conv2 && !(et < cbudget))) break;
-          if (conv2 && li == 0) SKIP_STAT(1, 1);
-          cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
-          ++it;
-        }
+        cert_stretch<T, DAMPED, SP>(m, prm.max_iters, prm.eps2, prm.dt, prm.lambda, arm, li, RT, tT, Rr, qcert,
+                                    cbudget, qc, qa, sn, cs, it);
         if (arm == 0) V.q[m->root_q] = qc;
         for (int k = 0; k < kArmDof; ++k) V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
       }
@@ -893,6 +938,7 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
     }
     const bool check = need && !known;
     if (li == 0 && check) SKIP_STAT(0, 1);
+    if (li == 0 && active) SKIP_STAT(7, 1);
     if (li == 0 && known) SKIP_STAT(1, 1);
     if (__any(check)) {
       const bool col = collide_group<T, LG>(m, c, V, li, lane0, check, gmask, prof);
@@ -1204,7 +1250,7 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
 extern "C" int ikg_debug_skip(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_skip), sizeof(g_skip)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[6] = {};
+    unsigned long long z[8] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_skip), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

@@ -28,7 +28,7 @@ lib.ikg_debug_cprof.argtypes = [C.c_void_p, C.c_int]
 lib.ikg_debug_skip.argtypes = [C.c_void_p, C.c_int]
 lib.ikg_debug_wprof.argtypes = [C.c_void_p, C.c_int]
 wp = np.zeros(6, np.uint64)
-sk = np.zeros(6, np.uint64)
+sk = np.zeros(8, np.uint64)
 tdt = torch.float64 if dtype == "f64" else torch.float32
 dev = torch.device("cuda", 0)
 tg = torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device=dev)
@@ -49,7 +49,7 @@ out = {k: int(v) for k, v in zip(names, buf)}
 out["cycles_per_iter"] = {k: round(int(buf[i]) / n_it, 1) for i, k in enumerate(names[:6])}
 out["success"] = int(sol.converged.sum().item())
 out["certificate"] = {k: int(v) for k, v in zip(["checks_run", "checks_known", "hit_with_tetra", "epa_runs",
-                                                   "epa_certified", "margin_sum_nm"], sk)}
+                                                   "epa_certified", "margin_sum_nm", "stretch_iters", "main_loop_iters"], sk)}
 out["witness_lane_cycles"] = {"gjk_per_call": int(wp[0]) // max(int(wp[3]), 1), "gjk_calls": int(wp[3]),
                                "certify_per_call": int(wp[1]) // max(int(wp[4]), 1), "certify_calls": int(wp[4]),
                                "epa_per_call": int(wp[2]) // max(int(wp[5]), 1)}
