@@ -470,7 +470,7 @@ __device__ double epa_depth_lb_group(const Shape<T>& A, const Shape<T>& B, const
 // joint origin + its bounding radius + twice the margin, which bounds that
 // distance over the motions the margin allows).
 template <typename T, int LG>
-__device__ __attribute__((noinline)) void certify_witness(int nq, Shape<T> A, Shape<T> B, Witness<T>& W,
+__device__ __attribute__((always_inline)) inline void certify_witness(int nq, Shape<T> A, Shape<T> B, Witness<T>& W,
                                                           const T (*Fa)[12], const int32_t* par, int li, int lane0) {
   const double tol = sizeof(T) == 8 ? 1e-9 : 1e-5;
 #ifdef IKG_CPROF
@@ -796,7 +796,9 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
                                                                   int32_t* __restrict__ witness, int handoff,
                                                                   int32_t* __restrict__ stretch_list,
                                                                   int32_t* __restrict__ stretch_count,
-                                                                  T* __restrict__ stretch_rec) {
+                                                                  T* __restrict__ stretch_rec,
+                                                                  const int32_t* __restrict__ cont_list,
+                                                                  const int32_t* __restrict__ cont_count) {
   extern __shared__ __align__(16) char lds[];
   constexpr int LG = 64 / G;
   const int lane = threadIdx.x;
@@ -804,7 +806,10 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
   const unsigned long long gmask = LG == 64 ? ~0ull : (((1ull << LG) - 1ull) << lane0);
   const int nq = m->nq;
   const GroupLds<T> V = group_view<T>(lds, g, nq, c->n_geoms);
-  const int64_t p = (int64_t)blockIdx.x * G + g;
+  // the pre-screen's colliding problems, compacted in problem order
+  // (ikg_compact_kernel): G per wave instead of ~G * fraction colliding
+  const int64_t slot = (int64_t)blockIdx.x * G + g;
+  const int64_t p = slot < (int64_t)*cont_count ? (int64_t)cont_list[slot] : B;
   // problems whose hand errors passed in the pair kernel and whose first
   // check collided (ikg_prescreen_kernel: the others are final, success)
   const bool started = p < B && conv[p] != 0 && witness[p] >= 0;
@@ -1095,6 +1100,33 @@ __global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* _
   }
 }
 
+// Problems the pre-screen left colliding (witness >= 0), listed in problem
+// order by one workgroup: contiguous chunks per thread, counted, scanned,
+// written.  Order-preserving, so the continuation's grouping (and with it the
+// results, bit for bit) does not depend on scheduling.
+__global__ __launch_bounds__(1024) void ikg_compact_kernel(const int32_t* __restrict__ witness, int64_t B,
+                                                           int32_t* __restrict__ list,
+                                                           int32_t* __restrict__ count) {
+  __shared__ int32_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t chunk = (B + 1023) / 1024;
+  const int64_t b0 = min(B, t * chunk), b1 = min(B, b0 + chunk);
+  int n = 0;
+  for (int64_t i = b0; i < b1; ++i) n += witness[i] >= 0;
+  part[t] = n;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int k = part[t] - n;
+  for (int64_t i = b0; i < b1; ++i)
+    if (witness[i] >= 0) list[k++] = (int32_t)i;
+  if (t == 1023) *count = part[1023];
+}
+
 // First check of the collision continuation for every problem whose errors
 // passed (inverse_geometry.py:70), one wave per problem (64 lanes per sweep,
 // against 16 in the continuation's groups): collision-free ones are final
@@ -1156,24 +1188,28 @@ static int cont_groups() {
 template <typename T>
 struct ContWs {
   int32_t* wit;
-  int32_t* list;
-  int32_t* count;
+  int32_t* list;    // stretch hand-off list
+  int32_t* count;   // its length; [1]: length of clist
+  int32_t* clist;   // the continuation's problems (ikg_compact_kernel)
   T* rec;
 };
 
 // Continuation launches that hand certified stretches to the stretch kernel
 // before the last one, which runs any remaining stretch itself.  Every round
 // is a grid-wide sync, and a problem whose margin runs out mid-stretch waits
-// for the round's longest stretch before its re-check: with few continued
-// problems (latency-bound, a wave or less per SIMD) the in-kernel stretch is
-// faster; with many (throughput-bound) the stretch kernel's 32 problems per
-// wave win.  Measured (tools/probe/rounds.sh, kernel ms per solve, 0/1/2
-// rounds): C2 fp64 B=4096: 2.47/3.45/3.17; C3 fp32 B=65536: 6.06/5.20/5.72.
-// IKG_HANDOFF_ROUNDS overrides (read per launch: the tests run both paths).
+// for the round's longest stretch before its re-check.  With the
+// continuation's problems compacted (4 per wave), the in-kernel stretch wins
+// at every measured size, so the default is 0 rounds.  Measured
+// (tools/probe/rounds.sh, kernel ms per solve, 0/1/2 rounds): C2 fp64
+// B=4096: 2.39/3.35/3.19; C3 fp32 B=65536: 5.10/5.38/5.71.  Before the
+// compaction (problems in place, ~0.5 per wave): C2 2.47/3.45/3.17, C3
+// 6.06/5.20/5.72.  IKG_HANDOFF_ROUNDS overrides (read per launch: the tests
+// run both paths).
 static int handoff_rounds(int64_t B) {
   const char* e = getenv("IKG_HANDOFF_ROUNDS");
   if (e) return std::min(64, std::max(0, atoi(e)));
-  return B > 16384 ? 1 : 0;
+  (void)B;
+  return 0;
 }
 
 // least problems per stretch wave (IKG_STRETCH_PPW; timing knob)
@@ -1199,7 +1235,7 @@ static void launch_continue_g(const KModel<T>* dm, const KCollision<T>* dc, cons
     if (handoff) (void)hipMemsetAsync(w.count, 0, sizeof(int32_t), s);
     hipLaunchKernelGGL((ikg_collide_continue_kernel<T, DAMPED, SP, G>), grid, dim3(64), lds, s, dm, dc, prm,
                        (const T*)a.targets, a.S, a.B, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, w.wit,
-                       handoff, w.list, w.count, w.rec);
+                       handoff, w.list, w.count, w.rec, (const int32_t*)w.clist, (const int32_t*)(w.count + 1));
     if (handoff)
       hipLaunchKernelGGL((ikg_cert_stretch_kernel<T, DAMPED, SP>), dim3(sgrid), dim3(64), 0, s, dm, prm,
                          (const T*)a.targets, a.S, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, w.wit,
@@ -1224,11 +1260,14 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
   // stream-ordered workspace: the pre-screen's witness pair per problem
   const size_t ib = ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255);
   char* ws = nullptr;
-  hipError_t e = hipMallocAsync((void**)&ws, 2 * ib + 256 + sizeof(T) * kStretchRec * (size_t)a.B, s);
+  hipError_t e = hipMallocAsync((void**)&ws, 3 * ib + 256 + sizeof(T) * kStretchRec * (size_t)a.B, s);
   if (e != hipSuccess) return e;
-  ContWs<T> w{(int32_t*)ws, (int32_t*)(ws + ib), (int32_t*)(ws + 2 * ib), (T*)(ws + 2 * ib + 256)};
+  ContWs<T> w{(int32_t*)ws, (int32_t*)(ws + ib), (int32_t*)(ws + 3 * ib), (int32_t*)(ws + 2 * ib),
+              (T*)(ws + 3 * ib + 256)};
   hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
                      (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
+  hipLaunchKernelGGL(ikg_compact_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)w.wit, a.B, w.clist,
+                     w.count + 1);
   const bool damped = prm.lambda > T(0);
   if (spec == kSpecNextage) {
     if (damped)

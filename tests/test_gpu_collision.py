@@ -67,7 +67,7 @@ def test_collision_batch_large_is_consistent(csolver, col_cases):
     assert np.array_equal(got, base)
 
 
-# continuation schedule: the size-based default, certified stretches run inside
+# continuation schedule: the default, certified stretches run inside
 # the continuation kernel (0 rounds), handed to ikg_cert_stretch_kernel (2)
 ROUNDS = [None, "0", "2"]
 
