@@ -886,22 +886,46 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
     // registers and pace) with its remaining margin; otherwise the stretch
     // runs here.  Either way it ends at the first iterate whose errors pass
     // once the margin is spent (redone below with a real check) or at max_iters.
-    if (active && li < 2 && cert_live && passive_clamped) {
-      if (handoff) {
-        if (li == 0) {
-          V.flag[3] = T(1);
-          stretch_rec[p * kStretchRec] = cbudget;
-        }
+    // the group's decision (its IK lanes'), for every lane of the group
+    const bool go_ik = active && li < 2 && cert_live && passive_clamped;
+    const bool go = __shfl(go_ik ? 1 : 0, lane0) != 0;
+    if (!handoff && go) {
+      // every lane of the group runs the stretch, the others mirroring their
+      // arm's IK lane bit for bit: a wave issues the same instruction stream
+      // either way, but with 2 live lanes out of 64 it ran 2.5x slower
+      // (tools/probe/mirror.sh); only the IK lanes keep the results
+      const int src = lane0 + arm;
+      qc = __shfl(qc, src);
 #pragma unroll
-        for (int k = 0; k < 7; ++k) {
-          stretch_rec[p * kStretchRec + 1 + 7 * arm + k] = Rr[k];
-          stretch_rec[p * kStretchRec + 15 + 7 * arm + k] = qcert[k];
-        }
-      } else {
-        cert_stretch<T, DAMPED, SP>(m, prm.max_iters, prm.eps2, prm.dt, prm.lambda, arm, li, RT, tT, Rr, qcert,
-                                    cbudget, qc, qa, sn, cs, it);
+      for (int k = 0; k < kArmDof; ++k) qa[k] = __shfl(qa[k], src);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        sn[k] = __shfl(sn[k], src);
+        cs[k] = __shfl(cs[k], src);
+        Rr[k] = __shfl(Rr[k], src);
+        qcert[k] = __shfl(qcert[k], src);
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) RT[k] = __shfl(RT[k], src);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) tT[k] = __shfl(tT[k], src);
+      cbudget = __shfl(cbudget, src);
+      cert_stretch<T, DAMPED, SP>(m, prm.max_iters, prm.eps2, prm.dt, prm.lambda, arm, li, RT, tT, Rr, qcert,
+                                  cbudget, qc, qa, sn, cs, it);
+      if (li < 2) {
         if (arm == 0) V.q[m->root_q] = qc;
         for (int k = 0; k < kArmDof; ++k) V.q[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
+      }
+    }
+    if (handoff && go_ik) {
+      if (li == 0) {
+        V.flag[3] = T(1);
+        stretch_rec[p * kStretchRec] = cbudget;
+      }
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        stretch_rec[p * kStretchRec + 1 + 7 * arm + k] = Rr[k];
+        stretch_rec[p * kStretchRec + 15 + 7 * arm + k] = qcert[k];
       }
     }
     if (handoff) {
@@ -1046,11 +1070,15 @@ __global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* _
   const int n = *stretch_count;
   const int lane = threadIdx.x, arm = lane & 1;
   const int nb = (int)gridDim.x;
-  const int ppw = min(32, max(ppw_min, (n + nb - 1) / nb));
+  // ppw_min < 0 (timing experiment): one problem per wave, every lane pair
+  // of the wave computing it, lanes 0/1 storing
+  const bool mirror = ppw_min < 0;
+  const int ppw = mirror ? 1 : min(32, max(ppw_min, (n + nb - 1) / nb));
+  const bool writer = !mirror || lane < 2;
   const int nq = m->nq;
   for (int base = (int)blockIdx.x * ppw; base < n; base += nb * ppw) {
-    const int i = base + (lane >> 1);
-    if (lane >= 2 * ppw || i >= n) continue;  // both lanes of a pair together
+    const int i = base + (mirror ? 0 : lane >> 1);
+    if ((!mirror && lane >= 2 * ppw) || i >= n) continue;  // both lanes of a pair together
     const int64_t p = stretch_list[i];
     const int64_t tgt = S_per_target > 1 ? p / S_per_target : p;
     T RT[9], tT[3], qc, qa[kArmDof], sn[7], cs[7], Rr[7], qcert[7];
@@ -1088,6 +1116,7 @@ __global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* _
       cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
       ++it;
     }
+    if (!writer) continue;
     if (arm == 0) qrow[m->root_q] = qc;
 #pragma unroll
     for (int k = 0; k < kArmDof; ++k) qrow[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
@@ -1217,7 +1246,8 @@ static int stretch_ppw() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("IKG_STRETCH_PPW");
-    v = e ? std::min(32, std::max(1, atoi(e))) : 32;
+    v = e ? std::min(32, std::max(-1, atoi(e))) : 32;
+    if (v == 0) v = 1;
   }
   return v;
 }
