@@ -135,3 +135,27 @@ def test_check_collision_without_scene_fails_loudly(solver):
     with pytest.raises(IkgError, match="collision scene"):
         solver.solve(np.concatenate([np.eye(3).reshape(9), [0.4, 0.1, 0.93]])[None], np.zeros(15),
                      check_collision=True)
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_solve_with_collision_is_deterministic_at_bench_size(csolver, dtype):
+    """C2's 4,096 uniform-sampler targets: the continuation's problem list is
+    compacted in problem order and certificates only skip checks whose answer
+    is known, so two solves agree bit for bit, and every problem reported
+    successful is collision-free while every converged-but-failed one collides."""
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(4096, seed=0)
+    a = csolver.solve(tg, np.zeros(15), dtype=dtype, check_collision=True)
+    b = csolver.solve(tg, np.zeros(15), dtype=dtype, check_collision=True)
+    assert np.array_equal(a.q, b.q) and np.array_equal(a.iters, b.iters)
+    assert np.array_equal(a.converged, b.converged) and np.array_equal(a.err, b.err)
+    free = csolver.solve(tg, np.zeros(15), dtype=dtype)
+    ran_on = free.converged.astype(bool) & ~a.converged.astype(bool)
+    assert a.converged.sum() > 0 and ran_on.sum() > 100
+    ok = a.converged.astype(bool)
+    free_ok = ~csolver.collision(a.q[ok], tg[ok], dtype=dtype)
+    hit = csolver.collision(a.q[ran_on], tg[ran_on], dtype=dtype)
+    if dtype == "f64":
+        assert free_ok.all() and hit.all()
+    else:  # fp32 GJK near touching contacts may answer differently by test order
+        assert free_ok.mean() >= 0.99 and hit.mean() >= 0.99
