@@ -1304,11 +1304,12 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
       launch_continue_t<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, w, s);
     else
       launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, nq, ng, w, s);
+  } else if (damped) {
+    launch_continue_t<T, true, SpecGeneric>(dm, dc, prm, a, nq, ng, w, s);
+  } else if (spec == kSpecGenericWrist) {
+    launch_continue_t<T, false, SpecGenericWrist>(dm, dc, prm, a, nq, ng, w, s);
   } else {
-    if (damped)
-      launch_continue_t<T, true, SpecGeneric>(dm, dc, prm, a, nq, ng, w, s);
-    else
-      launch_continue_t<T, false, SpecGeneric>(dm, dc, prm, a, nq, ng, w, s);
+    launch_continue_t<T, false, SpecGeneric>(dm, dc, prm, a, nq, ng, w, s);
   }
   e = hipGetLastError();
   const hipError_t ef = hipFreeAsync(ws, s);

@@ -97,6 +97,9 @@ struct Spec {
   static constexpr bool fold_hand = axis(7) != kAxRuntime && axis(7) == axis(6);
 };
 using SpecGeneric = Spec<kPatternGeneric, true, false>;
+// any model whose arm joints 3, 4, 5 meet in a point (ikg_model_build.hpp):
+// generic tables, the decoupled wrist solve instead of the 6x6 QR
+using SpecGenericWrist = Spec<kPatternGeneric, true, true>;
 // Nextage (NextageaOpen.urdf:580-730): root Z; arm Z,Y,Y,X,Y,Z; hand Rz(1.5708);
 // identity joint placements; spherical wrist at LARM/RARM_JOINT4.
 constexpr int kPatternNextage = 2 | (2 << 2) | (1 << 4) | (1 << 6) | (0 << 8) | (1 << 10) | (2 << 12) | (2 << 14);

@@ -128,14 +128,17 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
     col = &kc;
   }
   const ikg::KParams<T> prm = ikg::make_kparams<T>(p);
-  const bool special = p->variant != 99 && ikg::choose_spec(m) == 1;  // variant 99: force generic
+  const int spec = p->variant == 99 ? 0 : ikg::choose_spec(m);  // variant 99: force generic
   for (int64_t i = 0; i < B; ++i) {
     const T* tg = (const T*)targets + 12 * i;
     const T* qr = (const T*)q0 + stride * i;
     T* tr = trace ? (T*)trace + (int64_t)2 * trace_len * i : nullptr;
-    if (special)
+    if (spec == 1)
       emu_one<T, ikg::SpecNextage>(m, prm, p->lambda > 0, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
                                    (T*)err + 2 * i, tr, trace_len, col);
+    else if (spec == 2 && !(p->lambda > 0))
+      emu_one<T, ikg::SpecGenericWrist>(m, prm, false, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
+                                        (T*)err + 2 * i, tr, trace_len, col);
     else
       emu_one<T, ikg::SpecGeneric>(m, prm, p->lambda > 0, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
                                    (T*)err + 2 * i, tr, trace_len, col);

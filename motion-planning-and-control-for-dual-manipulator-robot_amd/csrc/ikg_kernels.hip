@@ -384,11 +384,12 @@ hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, con
       launch_pair_batch_t<T, true, SpecNextage>(dmodel, prm, a, s);
     else
       launch_pair_batch_t<T, false, SpecNextage>(dmodel, prm, a, s);
+  } else if (damped) {  // the damped solve does not use the wrist structure
+    launch_pair_batch_t<T, true, SpecGeneric>(dmodel, prm, a, s);
+  } else if (spec == kSpecGenericWrist) {
+    launch_pair_batch_t<T, false, SpecGenericWrist>(dmodel, prm, a, s);
   } else {
-    if (damped)
-      launch_pair_batch_t<T, true, SpecGeneric>(dmodel, prm, a, s);
-    else
-      launch_pair_batch_t<T, false, SpecGeneric>(dmodel, prm, a, s);
+    launch_pair_batch_t<T, false, SpecGeneric>(dmodel, prm, a, s);
   }
   return hipGetLastError();
 }

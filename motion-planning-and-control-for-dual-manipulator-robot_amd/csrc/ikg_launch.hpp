@@ -49,6 +49,7 @@ struct MultiArgs {
 // kernel specialisation chosen at model creation (ikg_model_build.hpp)
 constexpr int kSpecGeneric = 0;
 constexpr int kSpecNextage = 1;
+constexpr int kSpecGenericWrist = 2;  // generic tables, spherical-wrist solve
 
 template <typename T>
 hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,

@@ -12,6 +12,15 @@
 
 namespace ikg {
 
+// |t x a| <= 1e-14 |t| |a|: the line through the origin along a contains t
+inline bool parallel_or_zero(const double* t, const double* a) {
+  const double c[3] = {t[1] * a[2] - t[2] * a[1], t[2] * a[0] - t[0] * a[2], t[0] * a[1] - t[1] * a[0]};
+  const double nc = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+  const double nt = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+  const double na = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+  return nc <= 1e-14 * nt * na;
+}
+
 inline bool is_identity(const double* R) {
   for (int r = 0; r < 3; ++r)
     for (int c = 0; c < 3; ++c)
@@ -84,16 +93,20 @@ inline void build_kmodel(const ikg_model_desc& d, KModel<T>& k) {
       }
     }
   }
-  // spherical wrist: joint 4's origin on joint 3's axis, joint 5's axis
-  // through joint 4's origin (identity placement rotations)
+  // spherical wrist: the axes of arm joints 3, 4, 5 meet at joint 4's origin,
+  // i.e. joint 4's origin lies on joint 3's axis (t4 || e3 in joint 3's frame)
+  // and joint 5's axis passes through it (t5 || R5 e5 in joint 4's frame).
+  // Any placement rotations; parallel up to 1e-14 relative (a tilted URDF's
+  // rpy round trip leaves ~1e-17 m).
   k.wrist = 1;
   for (int a = 0; a < 2; ++a) {
     const int q3 = d.arm_q[a][3], q4 = d.arm_q[a][4], q5 = d.arm_q[a][5];
-    if (!is_identity(d.placement[q4]) || !is_identity(d.placement[q5])) k.wrist = 0;
-    for (int i = 0; i < 3; ++i) {
-      if (i != d.axis[q3] && d.placement[q4][9 + i] != 0.0) k.wrist = 0;
-      if (i != d.axis[q5] && d.placement[q5][9 + i] != 0.0) k.wrist = 0;
-    }
+    const double* P4 = d.placement[q4];
+    const double* P5 = d.placement[q5];
+    double e3[3] = {0.0, 0.0, 0.0}, a5[3];
+    e3[d.axis[q3]] = 1.0;
+    for (int i = 0; i < 3; ++i) a5[i] = P5[3 * i + d.axis[q5]];  // R5 e5 (row-major)
+    if (!parallel_or_zero(P4 + 9, e3) || !parallel_or_zero(P5 + 9, a5)) k.wrist = 0;
   }
   // zero placement offsets shared by both arms (Spec zero mask)
   k.zmask = 0;
@@ -139,7 +152,8 @@ template <typename T>
 inline int choose_spec(const KModel<T>& k) {
   if (k.pattern == kPatternNextage && k.rot_mask == 0 && k.wrist && (k.zmask & kZeroNextage) == kZeroNextage)
     return 1;  // kSpecNextage
-  return 0;                                                                   // kSpecGeneric
+  if (k.wrist) return 2;  // kSpecGenericWrist
+  return 0;  // kSpecGeneric
 }
 
 
