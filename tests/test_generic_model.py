@@ -84,10 +84,14 @@ def test_collision_geometries_follow_the_conjugated_frames(model, gc):
             np.testing.assert_allclose(np.concatenate([R.reshape(9), t]), ref, atol=1e-14, err_msg=name)
 
 
-def test_emulated_kernel_solves_tilted_robot(model, gc):
+@pytest.mark.parametrize("variant", [0, 99])
+def test_emulated_kernel_solves_tilted_robot(model, gc, variant):
     """The kernel's device functions (host emulator, generic path: runtime
-    axes, placement rotations, Householder QR) reproduce the raw-axis oracle:
-    same convergence flags and update counts, q within 1e-9."""
+    axes, placement rotations) reproduce the raw-axis oracle: same convergence
+    flags and update counts, q within 1e-9.  variant 0: the model's own
+    specialisation -- the tilted robot's wrist joints meet in a point, so the
+    decoupled wrist solve (SpecGenericWrist); 99: forced SpecGeneric, the 6x6
+    Householder QR."""
     emu = os.path.join(os.path.dirname(_lib.LIB_PATH), "libikgrasp_emu.so")
     if not os.path.exists(emu):
         pytest.skip("libikgrasp_emu.so not built")
@@ -98,6 +102,7 @@ def test_emulated_kernel_solves_tilted_robot(model, gc):
     tg, q0 = np.ascontiguousarray(gc["targets"]), np.ascontiguousarray(gc["q0"])
     B = len(tg)
     p = _lib.default_params()
+    p.variant = variant
     q, conv, it, err = np.empty((B, model.nq)), np.empty(B, np.uint8), np.empty(B, np.int32), np.empty((B, 2))
     assert lib.ikg_emu_solve(C.byref(desc), 0, tg.ctypes.data, q0.ctypes.data, model.nq, B, C.byref(p),
                              q.ctypes.data, conv.ctypes.data, it.ctypes.data, err.ctypes.data, None, 0, None) == 0
