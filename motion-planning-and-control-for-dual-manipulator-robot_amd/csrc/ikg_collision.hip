@@ -507,7 +507,6 @@ __device__ __attribute__((always_inline)) inline void certify_witness(int nq, Sh
   }
   if (li == 0) {
     W.budget = d;
-    W.Emot = 0.0;
     W.skip_ok = 1;
     ++W.gen;
   }
@@ -844,7 +843,6 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
       V.W->epa_wait = 0;
       V.W->gen = 0;
       V.W->budget = 0.0;
-      V.W->Emot = 0.0;
       V.flag[3] = T(0);
     }
   }
@@ -1234,11 +1232,9 @@ struct ContWs {
 // compaction (problems in place, ~0.5 per wave): C2 2.47/3.45/3.17, C3
 // 6.06/5.20/5.72.  IKG_HANDOFF_ROUNDS overrides (read per launch: the tests
 // run both paths).
-static int handoff_rounds(int64_t B) {
+static int handoff_rounds() {
   const char* e = getenv("IKG_HANDOFF_ROUNDS");
-  if (e) return std::min(64, std::max(0, atoi(e)));
-  (void)B;
-  return 0;
+  return e ? std::min(64, std::max(0, atoi(e))) : 0;
 }
 
 // least problems per stretch wave (IKG_STRETCH_PPW; timing knob)
@@ -1259,7 +1255,7 @@ static void launch_continue_g(const KModel<T>* dm, const KCollision<T>* dc, cons
   const dim3 grid((unsigned)((a.B + G - 1) / G));
   // stretch kernel: enough waves to give every SIMD of the chip one, at most
   const unsigned sgrid = (unsigned)std::min<int64_t>(1024, a.B);
-  const int rounds = handoff_rounds(a.B);
+  const int rounds = handoff_rounds();
   for (int r = 0; r <= rounds; ++r) {
     const int handoff = r < rounds;
     if (handoff) (void)hipMemsetAsync(w.count, 0, sizeof(int32_t), s);

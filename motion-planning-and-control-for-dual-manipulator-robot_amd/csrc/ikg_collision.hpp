@@ -66,9 +66,10 @@ struct EpaScratch {
 // Witness of the previous check of one problem (LDS): the colliding pair and,
 // when its GJK ended on an enclosing tetrahedron, the 4 search directions.
 // Continuation only: a certified penetration margin of the witness pair
-// (budget, from epa_depth_lb) and the motion bound accumulated against it
-// since (Emot = sum over updates of sum_j |dq_j| Rmot[j]); while Emot < budget
-// the pair provably still intersects, so the check's answer is known.
+// (budget, from epa_depth_lb) and the lever arms Rmot of its geometries; the
+// IK lanes keep the certified iterate and, while sum_j |q_j - qcert_j| Rmot[j]
+// stays below budget, the pair provably still intersects, so the check's
+// answer is known.
 template <typename T>
 struct Witness {
   int32_t pair;     // -1: none
@@ -78,7 +79,6 @@ struct Witness {
   int32_t gen;      // bumped whenever skip_ok / budget / Rmot change (the IK lanes cache them)
   int32_t epa_go;   // this check's hit asks for a certificate (continuation)
   double budget;
-  double Emot;
   T Rmot[kMaxNq];   // per joint: lever-arm bound of the two geometries about it
   T gbrad[2];
   EpaScratch epa;
