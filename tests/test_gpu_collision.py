@@ -159,3 +159,18 @@ def test_solve_with_collision_is_deterministic_at_bench_size(csolver, dtype):
         assert free_ok.all() and hit.all()
     else:  # fp32 GJK near touching contacts may answer differently by test order
         assert free_ok.mean() >= 0.99 and hit.mean() >= 0.99
+
+
+def test_solve_with_collision_small_and_empty_batches(csolver, solve_cases):
+    """B = 0, and single problems solved alone: same flags and update counts
+    as inside the fixture batch, q equal to rounding (a problem's group-mates
+    in the continuation only decide where its certified stretches pause, and a
+    paused iterate is redone in the world frame: ulp-level differences)."""
+    c = solve_cases
+    empty = csolver.solve(np.zeros((0, 12)), np.zeros(15), check_collision=True)
+    assert len(empty.q) == 0 and len(empty.converged) == 0
+    full = csolver.solve(c["targets"], c["q0"], check_collision=True)
+    for i in range(0, len(c["targets"]), max(1, len(c["targets"]) // 12)):
+        one = csolver.solve(c["targets"][i:i + 1], c["q0"][i:i + 1], check_collision=True)
+        assert one.converged[0] == full.converged[i] and one.iters[0] == full.iters[i]
+        assert np.abs(one.q[0] - full.q[i]).max() <= 1e-12
