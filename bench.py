@@ -129,7 +129,7 @@ def main():
             ev[0].record(stream)
         if S:
             solver.solve_multistart_into(targets, seeds, q_out, conv, iters, err, best, code, sh,
-                                         check_collision=args.collision)
+                                         variant=args.variant, check_collision=args.collision)
         else:
             solver.solve_into(targets, q0, q_out, conv, iters, err, code, sh, variant=args.variant,
                               check_collision=args.collision)
@@ -169,8 +169,9 @@ def main():
     # the batch kernel the C-ABI dispatches (ikg_kernels.hip launch_pair_batch): the packed fp32
     # layout from B >= 65,536 on 256 CUs (2 pair waves per SIMD), else the pair layout
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    # (multi-start: AUTO keeps the pair layout)
     packed = args.dtype == "f32" and (args.variant == _lib.IKG_VARIANT_PACKED or
-                                      (args.variant == _lib.IKG_VARIANT_AUTO and B * max(S, 1) >= cus * 4 * 2 * 32))
+                                      (args.variant == _lib.IKG_VARIANT_AUTO and not S and B >= cus * 4 * 2 * 32))
     kname = "ikg_packed_batch_kernel" if packed else "ikg_pair_batch_kernel"
     layout = "packed layout (both arms per lane, 64 problems/wave)" if packed else "pair layout (2 lanes/problem)"
     if rank == 0:

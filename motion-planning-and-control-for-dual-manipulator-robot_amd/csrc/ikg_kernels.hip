@@ -400,7 +400,11 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   if (a.T <= 0) return hipSuccess;
   // 1) every (target, seed) problem through the pair kernel into the workspace
   BatchArgs b{a.targets, a.seeds, a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
-  b.variant = a.variant;
+  // AUTO keeps the pair layout here: seeds spread the update counts, and a
+  // wave lasts as long as its slowest problem -- 64 per packed wave against 32
+  // per pair wave measured 4.17 ms against 3.66 ms (256 seeds x 512 targets,
+  // fp32, tools/probe/bisect_c5_trace.sh)
+  b.variant = a.variant == IKG_VARIANT_AUTO ? IKG_VARIANT_PAIR : a.variant;
   hipError_t e = launch_pair_batch<T>(dmodel, prm, b, spec, s);
   if (e != hipSuccess) return e;
   if (a.collision) {  // converged-but-colliding seeds keep iterating (inverse_geometry.py:70)
