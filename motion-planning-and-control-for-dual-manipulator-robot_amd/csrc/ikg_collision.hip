@@ -806,7 +806,7 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
   const int nq = m->nq;
   const GroupLds<T> V = group_view<T>(lds, g, nq, c->n_geoms);
   // the pre-screen's colliding problems, compacted in problem order
-  // (ikg_compact_kernel): G per wave instead of ~G * fraction colliding
+  // (ikg_compact_*_kernel): G per wave instead of ~G * fraction colliding
   const int64_t slot = (int64_t)blockIdx.x * G + g;
   const int64_t p = slot < (int64_t)*cont_count ? (int64_t)cont_list[slot] : B;
   // problems whose hand errors passed in the pair kernel and whose first
@@ -1128,30 +1128,59 @@ __global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* _
 }
 
 // Problems the pre-screen left colliding (witness >= 0), listed in problem
-// order by one workgroup: contiguous chunks per thread, counted, scanned,
-// written.  Order-preserving, so the continuation's grouping (and with it the
-// results, bit for bit) does not depend on scheduling.
-__global__ __launch_bounds__(1024) void ikg_compact_kernel(const int32_t* __restrict__ witness, int64_t B,
-                                                           int32_t* __restrict__ list,
-                                                           int32_t* __restrict__ count) {
-  __shared__ int32_t part[1024];
+// order: ikg_compact_count_kernel counts each block's chunk, then
+// ikg_compact_write_kernel adds the earlier chunks' counts and writes its
+// chunk's problems in rounds of 256 (wave ballots + a 4-wave prefix).
+// Order-preserving, so the continuation's grouping (and with it the results,
+// bit for bit) does not depend on scheduling.  Coalesced: one thread per
+// element per round (the single-workgroup form, one thread per contiguous
+// chunk, took 100 us at 131,072 problems).
+constexpr int kCompactChunk = 4096;
+
+__global__ __launch_bounds__(256) void ikg_compact_count_kernel(const int32_t* __restrict__ witness, int64_t B,
+                                                                int32_t* __restrict__ counts) {
+  __shared__ int32_t part[4];
   const int t = threadIdx.x;
-  const int64_t chunk = (B + 1023) / 1024;
-  const int64_t b0 = min(B, t * chunk), b1 = min(B, b0 + chunk);
+  const int64_t b0 = (int64_t)blockIdx.x * kCompactChunk, b1 = min(B, b0 + kCompactChunk);
   int n = 0;
-  for (int64_t i = b0; i < b1; ++i) n += witness[i] >= 0;
-  part[t] = n;
+  for (int64_t i = b0 + t; i < b1; i += 256) n += witness[i] >= 0;
+  n = __popcll(__ballot(n & 1)) + 2 * __popcll(__ballot(n & 2)) + 4 * __popcll(__ballot(n & 4)) +
+      8 * __popcll(__ballot(n & 8)) + 16 * __popcll(__ballot(n & 16));  // n <= 16 per thread
+  if ((t & 63) == 0) part[t >> 6] = n;
   __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan
-    const int v = t >= o ? part[t - o] : 0;
+  if (t == 0) counts[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+__global__ __launch_bounds__(256) void ikg_compact_write_kernel(const int32_t* __restrict__ witness, int64_t B,
+                                                                const int32_t* __restrict__ counts,
+                                                                int32_t* __restrict__ list,
+                                                                int32_t* __restrict__ count) {
+  __shared__ int32_t part[4];
+  __shared__ int32_t base;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (wv == 0) {  // offset of this chunk: the earlier chunks' counts
+    int s = 0;
+    for (int j = lane; j < (int)blockIdx.x; j += 64) s += counts[j];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) base = s;
+  }
+  __syncthreads();
+  int off = base;
+  const int64_t b0 = (int64_t)blockIdx.x * kCompactChunk, b1 = min(B, b0 + kCompactChunk);
+  const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int64_t r = b0; r < b1; r += 256) {
+    const int64_t i = r + t;
+    const bool f = i < b1 && witness[i] >= 0;
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) part[wv] = __popcll(m);
     __syncthreads();
-    part[t] += v;
+    int wo = off;
+    for (int k = 0; k < wv; ++k) wo += part[k];
+    if (f) list[wo + __popcll(m & below)] = (int32_t)i;
+    off += part[0] + part[1] + part[2] + part[3];
     __syncthreads();
   }
-  int k = part[t] - n;
-  for (int64_t i = b0; i < b1; ++i)
-    if (witness[i] >= 0) list[k++] = (int32_t)i;
-  if (t == 1023) *count = part[1023];
+  if (blockIdx.x == gridDim.x - 1 && t == 0) *count = off;
 }
 
 // First check of the collision continuation for every problem whose errors
@@ -1217,7 +1246,7 @@ struct ContWs {
   int32_t* wit;
   int32_t* list;    // stretch hand-off list
   int32_t* count;   // its length; [1]: length of clist
-  int32_t* clist;   // the continuation's problems (ikg_compact_kernel)
+  int32_t* clist;   // the continuation's problems (ikg_compact_*_kernel)
   T* rec;
 };
 
@@ -1292,8 +1321,12 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
               (T*)(ws + 3 * ib + 256)};
   hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
                      (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
-  hipLaunchKernelGGL(ikg_compact_kernel, dim3(1), dim3(1024), 0, s, (const int32_t*)w.wit, a.B, w.clist,
-                     w.count + 1);
+  {  // the chunk counts borrow the stretch list (written only after the compaction)
+    const unsigned nb = (unsigned)((a.B + kCompactChunk - 1) / kCompactChunk);
+    hipLaunchKernelGGL(ikg_compact_count_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)w.wit, a.B, w.list);
+    hipLaunchKernelGGL(ikg_compact_write_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)w.wit, a.B,
+                       (const int32_t*)w.list, w.clist, w.count + 1);
+  }
   const bool damped = prm.lambda > T(0);
   if (spec == kSpecNextage) {
     if (damped)
