@@ -135,6 +135,35 @@ def test_config_b65536_fp32_vs_fp64(solver):
     _check_reported_errors(solver, s32, tg, 2e-5)
 
 
+def test_config_c4_full_batch_fp64_shards_and_limits(solver):
+    """C4 at its full size (1,048,576 targets, fp64) on one GPU.  Size-independent
+    properties: the whole batch equals the concatenation of its 8 rank shards
+    (the weak-scaling partition of bench.py, bit-exact), every q is inside the URDF
+    limits (tools.py:21-22), non-converged problems ran all 1000 updates
+    (inverse_geometry.py:56), and the reported errors agree with an independent FK."""
+    from ikgrasp.parallel import shard_range
+    from ikgrasp.workload import uniform_targets
+    B = 1 << 20
+    tg = uniform_targets(B, seed=11)
+    full = solver.solve(tg, np.zeros(15), dtype="f64")
+    assert full.q.shape == (B, 15)
+    lo_lim, hi_lim = solver.model.lower, solver.model.upper
+    assert ((full.q >= lo_lim - 1e-15) & (full.q <= hi_lim + 1e-15)).all()
+    assert (full.iters[~full.converged] == 1000).all()
+    assert (full.err[full.converged] < 1e-3).all()
+    assert 0.3 < full.converged.mean() < 0.5  # the path.py sampler from q0 = 0 (DESIGN §5)
+    for r in (0, 3, 7):
+        lo, hi = shard_range(B, r, 8)
+        part = solver.solve(tg[lo:hi], np.zeros(15), dtype="f64")
+        assert np.array_equal(part.q, full.q[lo:hi])
+        assert np.array_equal(part.iters, full.iters[lo:hi])
+        assert np.array_equal(part.converged, full.converged[lo:hi])
+    idx = np.random.default_rng(0).choice(B, 4096, replace=False)
+    hands = solver.fk(full.q[idx])
+    err = helpers.hand_errors_from_fk(solver.model, hands, tg[idx])
+    assert np.abs(err - full.err[idx]).max() <= 1e-9
+
+
 # ---------------------------------------------------------------- edge cases
 def test_batch_position_invariance_and_ragged_sizes(solver):
     from ikgrasp.workload import uniform_targets
