@@ -24,75 +24,11 @@
 
 #include "ikg_device.hpp"
 #include "ikgrasp.h"
+#include "ikg_solve.hpp"
 #include "ikg_launch.hpp"
 
 namespace ikg {
 
-// Stop test of inverse_geometry.py:70 on squared norms (KParams::eps2):
-// pair layout = this lane's hand and the partner's; packed = both halves.
-template <typename T, typename E>
-__device__ inline bool both_below(T x, T xo, E eps2) {
-  if constexpr (is_packed<T>)
-    return all_of(x < T(eps2));
-  else
-    return x < eps2 && xo < eps2;
-}
-
-// One problem: run the reference loop to its stop condition.  T = double /
-// float: this lane owns one arm (pair layout, partner = lane ^ 1); T = v2f:
-// this lane owns both arms (packed layout).  Returns (through refs) the final
-// q of this lane, the update count and the hand error norms at the returned q.
-template <typename T, bool DAMPED, class SP>
-__device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
-                                  const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
-                                  T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out) {
-  static_assert(!(DAMPED && is_packed<T>), "the packed layout implements lambda = 0 only");
-  T sn[7], cs[7];
-  trig_exact(qc, qa, sn, cs);
-  int it = 0;
-  bool conv = false;
-  T x, xo;  // squared error norms of this lane's hand and the partner's
-  ThetaTrack<T> tk{};
-  for (;;) {
-    ArmState<T> st;
-    if constexpr (IKG_THETA_TRACK && is_f64<T>)  // fp32: atan2f is as cheap (measured)
-      x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, &tk, (it % Trig<T>::kResync) == 0);
-    else
-      x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
-    // the step is formed before the stop test (discarded when the loop ends)
-    // so the test's exchange/compare overlaps the solve instead of heading it
-    T dq[6], alpha, beta, s;
-    if constexpr (!DAMPED) {
-      T u[6], v[6];
-      arm_solve<T, SP>(st, u, v, alpha, beta);
-      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
-      arm_dq(u, v, s, dq);
-    } else {
-      T A[6][8], ze[6], zc[6];
-      arm_system(st, A);
-      arm_solve_damped(A, prm.lambda, ze, zc, alpha, beta);
-      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
-      arm_dq_damped(A, ze, zc, s, dq);
-    }
-    xo = pair_swap(x);
-    if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
-    if (both_below(x, xo, prm.eps2)) {  // |e_L| < eps and |e_R| < eps (:70)
-      conv = true;
-      break;
-    }
-    T q_old[7];
-    q_old[0] = qc;
-#pragma unroll
-    for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
-    arm_update(m, arm, T(prm.dt), s, dq, qc, qa);
-    ++it;
-    trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
-  }
-  it_out = it;
-  nrm_out = sqrt(x);
-  other_out = sqrt(xo);
-  conv_out = conv;
-}
 
 template <typename T>
 __device__ inline void load_q(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow, T& qc, T* qa) {
@@ -159,50 +95,6 @@ __global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __r
   if (err_out) err_out[p * 2 + arm] = nrm;
 }
 
-// Packed fp32 layout: one lane per problem, both arms in 2-vectors, so every
-// v_pk_{fma,mul,add}_f32 advances both arms and a wave holds 64 problems
-// (DESIGN.md §3).  Same loop, same arithmetic as the pair kernel's fp32 path.
-template <class SP>
-__global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
-                                                              KParams<float> prm, const float* __restrict__ targets,
-                                                              const float* __restrict__ q0, int64_t q0_stride,
-                                                              int64_t B, int64_t S, float* __restrict__ q_out,
-                                                              uint8_t* __restrict__ conv_out,
-                                                              int32_t* __restrict__ iters_out,
-                                                              float* __restrict__ err_out) {
-  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (p >= B) return;
-  const int64_t tgt = S > 1 ? p / S : p;
-  const int64_t row = S > 1 ? p - tgt * S : p;
-  v2f RT[9], tT[3];
-  hook_target_packed(m, targets + tgt * 12, RT, tT);
-  const float* qrow = q0 + row * q0_stride;
-  v2f qc = v2f(qrow[m->root_q]), qa[kArmDof];
-#pragma unroll
-  for (int k = 0; k < kArmDof; ++k) qa[k] = v2f{qrow[m->arm_q[0][k]], qrow[m->arm_q[1][k]]};
-  int it;
-  bool conv;
-  v2f nrm, other;
-  solve_pair<v2f, false, SP>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
-  float* qo = q_out + p * m->nq;
-  qo[m->root_q] = qc.x;
-  for (int i = 0; i < m->n_passive; ++i) {  // moved only by the first update's clamp (tools.py:21-22)
-    const int j = m->passive_q[i];
-    const float v = qrow[j];
-    qo[j] = it > 0 ? clampq(v, m->lo[j], m->hi[j]) : v;
-  }
-#pragma unroll
-  for (int k = 0; k < kArmDof; ++k) {
-    qo[m->arm_q[0][k]] = qa[k].x;
-    qo[m->arm_q[1][k]] = qa[k].y;
-  }
-  if (conv_out) conv_out[p] = conv ? 1 : 0;
-  if (iters_out) iters_out[p] = it;
-  if (err_out) {
-    err_out[p * 2] = nrm.x;
-    err_out[p * 2 + 1] = nrm.y;
-  }
-}
 
 // Multi-start best-seed reduction: one wave per target reduces the S seed
 // results the pair kernel wrote for it (key = worse hand error, converged
@@ -370,11 +262,7 @@ hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, con
   if constexpr (std::is_same<T, float>::value) {
     const bool want = a.variant == IKG_VARIANT_PACKED || (a.variant == IKG_VARIANT_AUTO && a.B >= packed_min_batch());
     if (want && packed_applies(prm, spec)) {
-      const dim3 grid((unsigned)((a.B + 63) / 64));
-      hipLaunchKernelGGL((ikg_packed_batch_kernel<SpecNextage>), grid, dim3(64), 0, s, dmodel, prm,
-                         (const float*)a.targets, (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out,
-                         a.converged, a.iters, (float*)a.err_out);
-      return hipGetLastError();
+      return launch_packed_batch(dmodel, prm, a, s);
     }
   }
   if (a.variant == IKG_VARIANT_PACKED) return hipErrorInvalidValue;  // checked by the C-ABI first

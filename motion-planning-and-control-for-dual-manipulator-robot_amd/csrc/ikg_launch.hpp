@@ -55,6 +55,10 @@ template <typename T>
 hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,
                              hipStream_t s);
 
+// packed fp32 layout, Nextage specialisation (ikg_packed.hip)
+hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>& prm, const BatchArgs& a,
+                               hipStream_t s);
+
 template <typename T>
 hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, int spec,
                              hipStream_t s);

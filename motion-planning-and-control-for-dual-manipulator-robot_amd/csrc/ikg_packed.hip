@@ -1,0 +1,69 @@
+// Packed fp32 IK kernel, in its own translation unit: it is built
+// with the max-ILP machine scheduler (one lane = both arms, 2-vector packed math;
+// latency-bound, so ILP beats the default occupancy-first schedule: 1.66 -> 1.49 us
+// per update at B = 65,536, while the same flag slows the fp64 pair kernel 17%
+// at B = 131,072, tools/ablate.py).
+#include <hip/hip_runtime.h>
+
+#include "ikg_device.hpp"
+#include "ikg_launch.hpp"
+#include "ikg_solve.hpp"
+#include "ikgrasp.h"
+
+namespace ikg {
+
+// Packed fp32 layout: one lane per problem, both arms in 2-vectors, so every
+// v_pk_{fma,mul,add}_f32 advances both arms and a wave holds 64 problems
+// (DESIGN.md §3).  Same loop, same arithmetic as the pair kernel's fp32 path.
+template <class SP>
+__global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
+                                                              KParams<float> prm, const float* __restrict__ targets,
+                                                              const float* __restrict__ q0, int64_t q0_stride,
+                                                              int64_t B, int64_t S, float* __restrict__ q_out,
+                                                              uint8_t* __restrict__ conv_out,
+                                                              int32_t* __restrict__ iters_out,
+                                                              float* __restrict__ err_out) {
+  const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (p >= B) return;
+  const int64_t tgt = S > 1 ? p / S : p;
+  const int64_t row = S > 1 ? p - tgt * S : p;
+  v2f RT[9], tT[3];
+  hook_target_packed(m, targets + tgt * 12, RT, tT);
+  const float* qrow = q0 + row * q0_stride;
+  v2f qc = v2f(qrow[m->root_q]), qa[kArmDof];
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) qa[k] = v2f{qrow[m->arm_q[0][k]], qrow[m->arm_q[1][k]]};
+  int it;
+  bool conv;
+  v2f nrm, other;
+  solve_pair<v2f, false, SP>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
+  float* qo = q_out + p * m->nq;
+  qo[m->root_q] = qc.x;
+  for (int i = 0; i < m->n_passive; ++i) {  // moved only by the first update's clamp (tools.py:21-22)
+    const int j = m->passive_q[i];
+    const float v = qrow[j];
+    qo[j] = it > 0 ? clampq(v, m->lo[j], m->hi[j]) : v;
+  }
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) {
+    qo[m->arm_q[0][k]] = qa[k].x;
+    qo[m->arm_q[1][k]] = qa[k].y;
+  }
+  if (conv_out) conv_out[p] = conv ? 1 : 0;
+  if (iters_out) iters_out[p] = it;
+  if (err_out) {
+    err_out[p * 2] = nrm.x;
+    err_out[p * 2 + 1] = nrm.y;
+  }
+}
+
+hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>& prm, const BatchArgs& a,
+                               hipStream_t s) {
+  const dim3 grid((unsigned)((a.B + 63) / 64));
+  hipLaunchKernelGGL((ikg_packed_batch_kernel<SpecNextage>), grid, dim3(64), 0, s, dmodel, prm,
+                     (const float*)a.targets, (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out,
+                     a.converged, a.iters, (float*)a.err_out);
+  return hipGetLastError();
+}
+
+}  // namespace ikg

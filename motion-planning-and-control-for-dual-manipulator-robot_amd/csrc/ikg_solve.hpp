@@ -1,0 +1,75 @@
+// The reference loop for one IK problem (inverse_geometry.py:56-94), shared by the
+// pair-layout kernels (ikg_kernels.hip) and the packed fp32 kernel (ikg_packed.hip,
+// its own translation unit so it can be compiled with a different scheduler).
+#pragma once
+#include "ikg_device.hpp"
+
+namespace ikg {
+
+// Stop test of inverse_geometry.py:70 on squared norms (KParams::eps2):
+// pair layout = this lane's hand and the partner's; packed = both halves.
+template <typename T, typename E>
+__device__ inline bool both_below(T x, T xo, E eps2) {
+  if constexpr (is_packed<T>)
+    return all_of(x < T(eps2));
+  else
+    return x < eps2 && xo < eps2;
+}
+
+// One problem: run the reference loop to its stop condition.  T = double /
+// float: this lane owns one arm (pair layout, partner = lane ^ 1); T = v2f:
+// this lane owns both arms (packed layout).  Returns (through refs) the final
+// q of this lane, the update count and the hand error norms at the returned q.
+template <typename T, bool DAMPED, class SP>
+__device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
+                                  const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
+                                  T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out) {
+  static_assert(!(DAMPED && is_packed<T>), "the packed layout implements lambda = 0 only");
+  T sn[7], cs[7];
+  trig_exact(qc, qa, sn, cs);
+  int it = 0;
+  bool conv = false;
+  T x, xo;  // squared error norms of this lane's hand and the partner's
+  ThetaTrack<T> tk{};
+  for (;;) {
+    ArmState<T> st;
+    if constexpr (IKG_THETA_TRACK && is_f64<T>)  // fp32: atan2f is as cheap (measured)
+      x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, &tk, (it % Trig<T>::kResync) == 0);
+    else
+      x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
+    // the step is formed before the stop test (discarded when the loop ends)
+    // so the test's exchange/compare overlaps the solve instead of heading it
+    T dq[6], alpha, beta, s;
+    if constexpr (!DAMPED) {
+      T u[6], v[6];
+      arm_solve<T, SP>(st, u, v, alpha, beta);
+      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+      arm_dq(u, v, s, dq);
+    } else {
+      T A[6][8], ze[6], zc[6];
+      arm_system(st, A);
+      arm_solve_damped(A, prm.lambda, ze, zc, alpha, beta);
+      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+      arm_dq_damped(A, ze, zc, s, dq);
+    }
+    xo = pair_swap(x);
+    if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
+    if (both_below(x, xo, prm.eps2)) {  // |e_L| < eps and |e_R| < eps (:70)
+      conv = true;
+      break;
+    }
+    T q_old[7];
+    q_old[0] = qc;
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
+    arm_update(m, arm, T(prm.dt), s, dq, qc, qa);
+    ++it;
+    trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
+  }
+  it_out = it;
+  nrm_out = sqrt(x);
+  other_out = sqrt(xo);
+  conv_out = conv;
+}
+
+}  // namespace ikg
