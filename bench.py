@@ -171,7 +171,7 @@ def main():
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     # (multi-start: AUTO keeps the pair layout)
     packed = args.dtype == "f32" and (args.variant == _lib.IKG_VARIANT_PACKED or
-                                      (args.variant == _lib.IKG_VARIANT_AUTO and not S and B >= cus * 4 * 2 * 32))
+                                      (args.variant == _lib.IKG_VARIANT_AUTO and not S and B > cus * 4 * 32))
     kname = "ikg_packed_batch_kernel" if packed else "ikg_pair_batch_kernel"
     layout = "packed layout (both arms per lane, 64 problems/wave)" if packed else "pair layout (2 lanes/problem)"
     if rank == 0:

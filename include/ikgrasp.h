@@ -55,7 +55,7 @@ enum ikg_status {
 
 /* kernel variant selector (ikg_params.variant) */
 enum ikg_variant {
-  IKG_VARIANT_AUTO = 0,   /* ikg_solve_batch: PACKED where it applies and B >= 8 pair waves per CU,
+  IKG_VARIANT_AUTO = 0,   /* ikg_solve_batch: PACKED where it applies and B > 4 pair waves per CU,
                              else PAIR; ikg_solve_multistart: PAIR */
   IKG_VARIANT_PAIR = 1,   /* two lanes per problem (one arm per lane), 32 problems / wave */
   IKG_VARIANT_PACKED = 2  /* fp32, Nextage-class models, lambda = 0: one lane per problem with

@@ -235,9 +235,10 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
 // The packed layout applies to fp32, the compiled Nextage specialisation and
 // lambda = 0.  It halves the instructions per problem but v_pk_fma_f32 issues
 // at ~4.4 cycles against ~2.7 for v_fma_f32 (tools/ubench/pkl.hip), and it
-// halves the waves: measured faster only once the pair layout would hold >= 2
-// waves per SIMD (B >= 65536 on 256 CUs: -8%, B = 4096: +30%).  AUTO takes it
-// from there on.
+// halves the waves: measured faster only once the pair layout would need a
+// second wave on some SIMD (B > 32768 on 256 CUs).  With the max-ILP build of
+// ikg_packed.hip: B = 32768 pair 1.22 ms / packed 1.47, B = 49152 1.78 / 1.46,
+// B = 65536 1.81 / 1.53 (bench.py, gpurun_out/thr).  AUTO takes it from there on.
 template <typename T>
 bool packed_applies(const KParams<T>& prm, int spec) {
   return std::is_same<T, float>::value && spec == kSpecNextage && !(prm.lambda > T(0));
@@ -250,7 +251,7 @@ static int64_t packed_min_batch() {
     if (hipGetDevice(&dev) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
-    v = (int64_t)cus * 4 /* SIMDs */ * 2 /* waves */ * 32 /* problems per pair wave */;
+    v = (int64_t)cus * 4 /* SIMDs */ * 32 /* problems per pair wave */ + 1;
   }
   return v;
 }
