@@ -170,6 +170,11 @@ void free_slots(std::vector<void*>& slot) {
 // sparser waves was 1.3-3x SLOWER (profiles/r01/ppw_sweep.txt).
 int auto_ppw(int /*device*/, int64_t /*B*/) { return 32; }
 
+// One-wave-per-problem kernels (collision query, pre-screen, continuation,
+// distance, best-seed) launch one 64-lane workgroup per unit; HIP caps a grid at
+// 2^32 - 1 work items, so a launch holds at most this many waves.
+constexpr int64_t kMaxWaves = (int64_t)0xFFFFFFFFu / 64;
+
 int check_params(const ikg_params* p) {
   if (!p) return fail(IKG_EINVAL, "params is NULL");
   if (!(p->eps > 0) || !std::isfinite(p->eps)) return fail(IKG_EINVAL, "eps must be > 0");
@@ -498,7 +503,13 @@ int ikg_solve_batch(const ikg_model* model, int device, int dtype, const void* t
   if (q0_stride != 0 && q0_stride < model->desc.nq) return fail(IKG_EINVAL, "q0_stride must be 0 or >= nq");
   if (int rc = check_params(params)) return rc;
   if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
-  if (params->check_collision && B > 0x7fffffff) return fail(IKG_EINVAL, "B too large for the collision launch");
+  {
+    const int ppw = params->problems_per_wave > 0 ? params->problems_per_wave : 32;
+    if ((B + ppw - 1) / ppw > kMaxWaves) return fail(IKG_EINVAL, "B=%lld too large for one launch", (long long)B);
+  }
+  if (params->check_collision && B > kMaxWaves)
+    return fail(IKG_EINVAL, "B=%lld too large for the collision launch (at most %lld)", (long long)B,
+                (long long)kMaxWaves);
   DeviceGuard g(device);
   if (g.rc) return g.rc;
   if (B == 0) return IKG_OK;
@@ -520,7 +531,11 @@ int ikg_solve_multistart(const ikg_model* model, int device, int dtype, const vo
   if (T > 0 && (!targets || !seeds || !q_out)) return fail(IKG_EINVAL, "targets, seeds and q_out are required");
   if (int rc = check_params(params)) return rc;
   if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
-  if (params->check_collision && T * S > 0x7fffffff) return fail(IKG_EINVAL, "T*S too large for the collision launch");
+  if (T > kMaxWaves || (T * S + 31) / 32 > kMaxWaves)
+    return fail(IKG_EINVAL, "T=%lld x S=%lld too large for one launch", (long long)T, (long long)S);
+  if (params->check_collision && T * S > kMaxWaves)
+    return fail(IKG_EINVAL, "T*S=%lld too large for the collision launch (at most %lld)", (long long)(T * S),
+                (long long)kMaxWaves);
   DeviceGuard g(device);
   if (g.rc) return g.rc;
   if (T == 0) return IKG_OK;
@@ -590,7 +605,7 @@ int ikg_collision_batch(const ikg_model* model, int device, int dtype, const voi
   if (B > 0 && (!q || !targets || !in_collision)) return fail(IKG_EINVAL, "q, targets and in_collision are required");
   if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
   if (!model->has_collision) return fail(IKG_EINVAL, "no collision scene attached (ikg_model_set_collision)");
-  if (B > 0x7fffffff) return fail(IKG_EINVAL, "B too large for one launch");
+  if (B > kMaxWaves) return fail(IKG_EINVAL, "B=%lld too large for one launch (at most %lld)", (long long)B, (long long)kMaxWaves);
   DeviceGuard g(device);
   if (g.rc) return g.rc;
   if (B == 0) return IKG_OK;
@@ -672,7 +687,7 @@ int ikg_distance_batch(const ikg_model* model, int device, int dtype, const void
   for (int32_t k = 0; k < n_pairs; ++k)
     if (pair_idx[k] < 0 || pair_idx[k] >= model->c64.n_pairs)
       return fail(IKG_EINVAL, "pair_idx[%d] = %d outside [0, %d)", k, pair_idx[k], model->c64.n_pairs);
-  if (B > 0x7fffffff) return fail(IKG_EINVAL, "B too large for one launch");
+  if (B > kMaxWaves) return fail(IKG_EINVAL, "B=%lld too large for one launch (at most %lld)", (long long)B, (long long)kMaxWaves);
   DeviceGuard g(device);
   if (g.rc) return g.rc;
   if (B == 0) return IKG_OK;

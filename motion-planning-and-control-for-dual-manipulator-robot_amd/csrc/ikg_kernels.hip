@@ -19,6 +19,7 @@
 // No LDS, no barriers; the model tables are read with uniform scalar loads.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -132,6 +133,9 @@ __global__ __launch_bounds__(256) void ikg_best_seed_kernel(int64_t T_, int64_t 
       best = oi;
     }
   }
+  // every key NaN (a non-finite target or seed): no seed wins the compare, so
+  // fall back to seed 0 rather than index past the target's S results
+  if (best >= S) best = 0;
   const int64_t k = tgt * S + best;
   for (int j = lane; j < nq; j += 64) q_out[tgt * nq + j] = q_all[k * nq + j];
   if (lane == 0) {
@@ -244,15 +248,22 @@ bool packed_applies(const KParams<T>& prm, int spec) {
   return std::is_same<T, float>::value && spec == kSpecNextage && !(prm.lambda > T(0));
 }
 
+// Per device (the launch's current device): CU counts may differ between
+// devices; the cache is filled racily but every writer stores the same value.
 static int64_t packed_min_batch() {
-  static int64_t v = -1;
-  if (v < 0) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    v = (int64_t)cus * 4 /* SIMDs */ * 32 /* problems per pair wave */ + 1;
+  constexpr int kDevs = 64;
+  static std::atomic<int64_t> cache[kDevs];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+  if (dev >= 0 && dev < kDevs) {
+    const int64_t v = cache[dev].load(std::memory_order_relaxed);
+    if (v > 0) return v;
   }
+  int cus = 256;
+  if (dev < 0 || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  const int64_t v = (int64_t)cus * 4 /* SIMDs */ * 32 /* problems per pair wave */ + 1;
+  if (dev >= 0 && dev < kDevs) cache[dev].store(v, std::memory_order_relaxed);
   return v;
 }
 
@@ -288,7 +299,9 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
                              hipStream_t s) {
   if (a.T <= 0) return hipSuccess;
   // 1) every (target, seed) problem through the pair kernel into the workspace
-  BatchArgs b{a.targets, a.seeds, a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
+  // S == 1: the one seed row serves every target (broadcast), since the batch
+  // kernel indexes q0 rows by problem when S == 1
+  BatchArgs b{a.targets, a.seeds, a.S == 1 ? 0 : a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
   // AUTO keeps the pair layout here: seeds spread the update counts, and a
   // wave lasts as long as its slowest problem -- 64 per packed wave against 32
   // per pair wave measured 4.17 ms against 3.66 ms (256 seeds x 512 targets,

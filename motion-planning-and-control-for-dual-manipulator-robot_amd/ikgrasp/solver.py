@@ -38,6 +38,18 @@ def _is_torch(x) -> bool:
     return type(x).__module__.startswith("torch")
 
 
+def _q0_stride(shape, B: int, nq: int) -> int:
+    """Row stride of a q0 array for ikg_solve_batch: [nq] or [1, nq] broadcast
+    (stride 0), [B, nq] one row per target (stride nq).  Anything else would
+    make the kernel read past the end of q0, so it is rejected here."""
+    shape = tuple(shape)
+    if shape == (nq,) or shape == (1, nq):
+        return 0
+    if shape == (B, nq):
+        return nq
+    raise ValueError(f"q0 must be [{nq}], [1,{nq}] or [{B},{nq}], got {list(shape)}")
+
+
 @dataclass
 class Solution:
     q: object            # [B, nq]
@@ -102,11 +114,7 @@ class IKSolver:
         tg = np.ascontiguousarray(targets, dtype=npt).reshape(-1, 12)
         B = tg.shape[0]
         q = np.ascontiguousarray(q0, dtype=npt)
-        stride = 0 if q.ndim == 1 else self.nq
-        if q.ndim == 2 and q.shape != (B, self.nq):
-            raise ValueError(f"q0 must be [{self.nq}] or [{B},{self.nq}], got {q.shape}")
-        if q.ndim == 1 and q.shape != (self.nq,):
-            raise ValueError(f"q0 must have {self.nq} entries")
+        stride = _q0_stride(q.shape, B, self.nq)
         q_out = np.empty((B, self.nq), dtype=npt)
         conv = np.empty(B, dtype=np.uint8)
         iters = np.empty(B, dtype=np.int32)
@@ -126,7 +134,7 @@ class IKSolver:
         tg = targets.contiguous().view(-1, 12)
         B = tg.shape[0]
         q = q0.to(device=dev, dtype=targets.dtype).contiguous()
-        stride = 0 if q.dim() == 1 else self.nq
+        stride = _q0_stride(q.shape, B, self.nq)
         q_out = torch.empty((B, self.nq), dtype=targets.dtype, device=dev)
         conv = torch.empty(B, dtype=torch.uint8, device=dev)
         iters = torch.empty(B, dtype=torch.int32, device=dev)
@@ -140,7 +148,7 @@ class IKSolver:
     def solve_into(self, targets, q0, q_out, conv, iters, err, dtype_code, stream_handle, **kw):
         """Raw device-pointer launch (all tensors preallocated; used by bench.py)."""
         prm = self.params(**kw)
-        stride = 0 if q0.dim() == 1 else self.nq
+        stride = _q0_stride(q0.shape, targets.shape[0], self.nq)
         _lib.check(self.lib.ikg_solve_batch(
             self._h, targets.device.index or 0, dtype_code, targets.data_ptr(), q0.data_ptr(), stride,
             targets.shape[0], C.byref(prm), q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(),
@@ -149,6 +157,8 @@ class IKSolver:
     def solve_multistart_into(self, targets, seeds, q_out, conv, iters, err, best, dtype_code, stream_handle, **kw):
         """Raw device-pointer multi-start launch (preallocated torch tensors; bench.py)."""
         prm = self.params(**kw)
+        if seeds.dim() != 2 or seeds.shape[1] != self.nq:
+            raise ValueError(f"seeds must be [S,{self.nq}], got {list(seeds.shape)}")
         _lib.check(self.lib.ikg_solve_multistart(
             self._h, targets.device.index or 0, dtype_code, targets.data_ptr(), targets.shape[0], seeds.data_ptr(),
             seeds.shape[0], C.byref(prm), q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(), err.data_ptr(),
@@ -271,6 +281,9 @@ class IKSolver:
             prep = lambda x: None if x is None else x.to(device=dev, dtype=q.dtype).contiguous().view(-1, nq)
             qq, vv, qd, vd = prep(q), prep(v), prep(q_des), prep(v_des)
             B = qq.shape[0]
+            for name, x in (("v", vv), ("q_des", qd), ("v_des", vd)):
+                if x is not None and x.shape[0] != B:
+                    raise ValueError(f"{name} has {x.shape[0]} rows, q has {B}")
             res = {k: torch.empty((B,) + shapes[k], dtype=q.dtype, device=dev) for k in outputs}
             ptr = lambda x: None if x is None else x.data_ptr()
             out = _lib.FrameKinOut(*[ptr(res.get(k)) for k in self.FRAME_KIN_OUTPUTS])

@@ -77,7 +77,31 @@ def test_solve_rejects_bad_arguments_before_touching_the_device():
     assert rc == -1 and "dtype" in lib.ikg_last_error().decode()
     rc = lib.ikg_solve_multistart(h, 0, 0, buf, 1, buf, 0, C.byref(p), buf, None, None, None, None, None, 0)
     assert rc == -1 and "S >= 1" in lib.ikg_last_error().decode()
+    # launch-size limits are checked before any device work (HIP caps a grid at
+    # 2^32 - 1 work items; the collision kernels run one 64-lane wave per problem)
+    p.check_collision = 1
+    big = (1 << 26) + 1
+    rc = lib.ikg_solve_batch(h, 0, 0, buf, buf, 0, big, C.byref(p), buf, None, None, None, None, 0)
+    assert rc == -1 and "too large" in lib.ikg_last_error().decode()
+    rc = lib.ikg_solve_multistart(h, 0, 0, buf, 1 << 13, buf, 1 << 13, C.byref(p), buf, None, None, None, None,
+                                  None, 0)
+    assert rc == -1 and "too large" in lib.ikg_last_error().decode()
+    p = _lib.default_params()
+    p.problems_per_wave = 1
+    rc = lib.ikg_solve_batch(h, 0, 0, buf, buf, 0, big, C.byref(p), buf, None, None, None, None, 0)
+    assert rc == -1 and "too large" in lib.ikg_last_error().decode()
     lib.ikg_model_destroy(h)
+
+
+def test_q0_shape_checks():
+    import numpy as np
+    from ikgrasp.solver import _q0_stride
+    assert _q0_stride((15,), 8, 15) == 0
+    assert _q0_stride((1, 15), 8, 15) == 0
+    assert _q0_stride((8, 15), 8, 15) == 15
+    for bad in ((2, 15), (8, 14), (14,), (8, 15, 1)):
+        with pytest.raises(ValueError):
+            _q0_stride(bad, 8, 15)
 
 
 def test_no_device_fails_loudly_without_gpu():

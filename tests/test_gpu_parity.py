@@ -252,6 +252,45 @@ def test_multistart_selects_best_seed(solver):
         assert ms.converged[t] == full.converged[k] and ms.iters[t] == full.iters[k]
 
 
+@pytest.mark.parametrize("variant", [1, 2])  # PAIR, PACKED
+def test_multistart_single_seed_broadcasts(solver, variant):
+    """S = 1 with T > 1: the one seed serves every target (the kernel
+    read seed rows past the end of the buffer)."""
+    from ikgrasp.workload import uniform_targets, random_seeds
+    dtype = "f32" if variant == 2 else "f64"
+    tg = uniform_targets(70, seed=21)
+    seed = random_seeds(solver.model, 1, seed=22)
+    ms = solver.solve_multistart(tg, seed, dtype=dtype, variant=variant)
+    ref = solver.solve(tg, seed[0], dtype=dtype, variant=variant)
+    assert np.array_equal(ms.q, ref.q) and np.array_equal(ms.iters, ref.iters)
+    assert np.array_equal(ms.converged, ref.converged) and (ms.best_seed == 0).all()
+
+
+def test_multistart_nan_target_picks_a_valid_seed(solver):
+    """Every seed of a NaN target has a NaN error: the best-seed reduction must
+    still pick a seed of that target (seed 0), not index past its results."""
+    from ikgrasp.workload import uniform_targets, random_seeds
+    tg = uniform_targets(3, seed=23)
+    tg[1, 9] = np.nan
+    seeds = random_seeds(solver.model, 5, seed=24)
+    ms = solver.solve_multistart(tg, seeds, dtype="f64", max_iters=20)
+    assert ms.best_seed[1] == 0 and not ms.converged[1]
+    ok = solver.solve_multistart(tg[[0, 2]], seeds, dtype="f64", max_iters=20)
+    assert np.array_equal(ms.q[[0, 2]], ok.q) and np.array_equal(ms.best_seed[[0, 2]], ok.best_seed)
+
+
+def test_torch_q0_shapes_are_checked(solver):
+    import torch
+    from ikgrasp.workload import uniform_targets
+    tg = torch.from_numpy(uniform_targets(8, seed=25)).cuda()
+    a = solver.solve(tg, torch.zeros(15, dtype=torch.float64))
+    b = solver.solve(tg, torch.zeros(1, 15, dtype=torch.float64))  # [1, nq] broadcasts
+    assert torch.equal(a.q, b.q)
+    for bad in ((2, 15), (8, 14), (8, 15, 1)):
+        with pytest.raises(ValueError):
+            solver.solve(tg, torch.zeros(*bad, dtype=torch.float64))
+
+
 def test_problems_per_wave_does_not_change_results(solver):
     from ikgrasp.workload import uniform_targets
     tg = uniform_targets(300, seed=9)

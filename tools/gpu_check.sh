@@ -16,7 +16,7 @@ stop_if_fatal() {  # $1 = exit code, $2 = step name
 }
 
 echo "== pytest -m gpu" | tee "$OUT/summary.txt"
-timeout -k 10 900 python -m pytest tests -m gpu -x -q > "$OUT/pytest_gpu_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/pytest_gpu_$TAG.log" 2>&1
 rc=$?; tail -5 "$OUT/pytest_gpu_$TAG.log" | tee -a "$OUT/summary.txt"; stop_if_fatal $rc pytest
 
 echo "== smoke" | tee -a "$OUT/summary.txt"
