@@ -26,6 +26,21 @@
 #ifndef IKG_THETA
 #define IKG_THETA 0
 #endif
+// log6's small-angle series by multiplications instead of divisions
+#ifndef IKG_TAYLOR_MUL
+#define IKG_TAYLOR_MUL 1
+#endif
+// pair kernel: per-lane joint limits held in registers (12 fp64) instead of
+// clamping against both arms' scalar limits and selecting
+#ifndef IKG_LANE_LIMITS
+#define IKG_LANE_LIMITS 1
+#endif
+// Nextage-pattern models: iterate in the frame of the first arm joint with the
+// closed-form arm solve (arm_fk_error_f1 / arm_solve_f1) instead of the chest
+// frame and the two 3x3 Cramer solves
+#ifndef IKG_FRAME1
+#define IKG_FRAME1 1
+#endif
 // carry the rotation angle across iterations (ThetaTrack)
 #ifndef IKG_THETA_TRACK
 #define IKG_THETA_TRACK 1
@@ -592,8 +607,16 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
   }
   T beta;
   if constexpr (is_f64<T>) {
+#if IKG_TAYLOR_MUL
+    // Pinocchio's series terms t2/12, t2^2/720 as products with the rounded
+    // reciprocals (<= 1 ulp of each term; the branch serves theta < 1.2e-4):
+    // three IEEE divisions (~11 instructions each) leave the loop
+    const T as = T(1) - t2 * T(1.0 / 12) - (t2 * t2) * T(1.0 / 720);
+    const T bs = T(1.0 / 12) + t2 * T(1.0 / 720);
+#else
     const T as = T(1) - t2 / T(12) - t2 * t2 / T(720);
     const T bs = T(1) / T(12) + t2 / T(720);
+#endif
     beta = vsel<T>(below, bs, (T(1) - alpha) * inv_t2);
     alpha = vsel<T>(below, as, alpha);
   } else {
@@ -1150,6 +1173,176 @@ IKG_HD inline void arm_solve(const ArmState<T>& st, T* u, T* v, T& alpha, T& bet
   }
 }
 
+// ---------------------------------------------------------------- frame-1 closed form
+// For the Nextage joint pattern (root Z; arm Z | Y Y | X Y Z; no placement
+// rotations; hand rotation about the last axis; spherical wrist at the origin
+// w of arm joint 4, ikg_model_build.hpp) the iteration runs in "frame 1": the
+// frame of arm joint 0 after its rotation.  There the arm's axes are constant
+// or nearly so,
+//   a_0 = e_z, a_1 = a_2 = e_y (o_0 = 0, o_1 = p_1),
+//   [a_3 a_4 a_5] = Ry(q1 + q2) [e_x, Rx(q3) e_y, Rx(q3) Ry(q4) e_z],
+// so the wrist-decoupled solve of arm_solve_wrist,
+//   G x_top = b_lin(w),  H x_bot = b_ang - F x_top,
+//   G = [a_j x (w - o_j)]_{j<3}, F = [a_j]_{j<3}, H = [a_j]_{j>=3},
+// has closed forms: G = [(-w_y, w_x, 0), (P1z, 0, -P1x), (P2z, 0, -P2x)] with
+// P_j = w - o_j (one scalar row, then a 2x2), and H = Ry(q12) H'' with
+// H'' = [[1, 0, s4], [0, c3, -s3 c4], [0, s3, c3 c4]] (a rotation, then 1/c4).
+// The arm joint 0 and root rotations are both about z, so the target is moved
+// into frame 1 by Rz(q_root + q_0)^T.  Same minimum-norm step as the chest-frame
+// path (pinv(J) e is invariant to the frame J and e are written in, and the
+// joint-space u, v are the same): ~100 fewer fp64 operations per update.
+template <class SP>
+constexpr bool kFrame1 = IKG_FRAME1 && SP::axis(0) == 2 && SP::axis(1) == 2 && SP::axis(2) == 1 &&
+                         SP::axis(3) == 1 && SP::axis(4) == 0 && SP::axis(5) == 1 && SP::axis(6) == 2 &&
+                         !SP::prot && SP::wrist && SP::fold_hand;
+
+template <typename T>
+struct ArmStateF1 {
+  T w[3];      // wrist centre = origin of arm joint 4
+  T o2[3];     // origin of arm joint 2
+  T c12, s12;  // rotation after arm joint 2: Ry(q1 + q2)
+  T k[2];      // (x, y) of Rz(q0)^T p_0: the root joint sits at -(k, p_0z)
+  T h[3];      // hand point
+  T e[6];      // pose error in frame-1 axes
+};
+
+// FK + pose error in frame 1 (inverse_geometry.py:58-67); returns |e|^2.
+// sn/cs slots: 0 root, 1..6 arm joints 0..5.
+template <typename T, class SP>
+IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const T* sn, const T* cs,
+                                const T* RT, const T* tT, ArmStateF1<T>& st, ThetaTrack<T>* tk, bool resync) {
+  static_assert(kFrame1<SP>, "frame-1 path needs the Nextage joint pattern");
+  const bool right = arm != 0;
+  // frame 1 = chest Rz(q_root) at root_t, then arm joint 0 at p_0 with Rz(q_0)
+  const T sf = sn[0] * cs[1] + cs[0] * sn[1];
+  const T cf = cs[0] * cs[1] - sn[0] * sn[1];
+  T p0[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) p0[i] = SP::zero_t(0, i) ? T(0) : armc<T>(right, m->arm_t[0][0][i], m->arm_t[1][0][i]);
+  st.k[0] = cs[1] * p0[0] + sn[1] * p0[1];
+  st.k[1] = cs[1] * p0[1] - sn[1] * p0[0];
+  T RT1[9], tT1[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    RT1[c] = cf * RT[c] + sf * RT[3 + c];
+    RT1[3 + c] = cf * RT[3 + c] - sf * RT[c];
+    RT1[6 + c] = RT[6 + c];
+  }
+  const T d0 = tT[0] - m->root_t[0], d1 = tT[1] - m->root_t[1];
+  tT1[0] = cf * d0 + sf * d1 - st.k[0];
+  tT1[1] = cf * d1 - sf * d0 - st.k[1];
+  tT1[2] = tT[2] - m->root_t[2] - p0[2];
+  // FK from arm joint 1 (R = I, origin of joint 0 at 0)
+  T R[9] = {T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)};
+  T t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) t[i] = SP::zero_t(1, i) ? T(0) : armc<T>(right, m->arm_t[0][1][i], m->arm_t[1][1][i]);
+  auto offset = [&](int k) {
+    T pt[3], d[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) pt[i] = SP::zero_t(k, i) ? T(0) : armc<T>(right, m->arm_t[0][k][i], m->arm_t[1][k][i]);
+    matvec3(R, pt, d);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t[i] += d[i];
+  };
+  rotate_axis(R, 1, sn[2], cs[2]);  // arm joint 1 (Y)
+  offset(2);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) st.o2[i] = t[i];
+  rotate_axis(R, 1, sn[3], cs[3]);  // arm joint 2 (Y): R = Ry(q1 + q2)
+  st.c12 = R[0];
+  st.s12 = R[2];
+  offset(3);
+  rotate_axis(R, 0, sn[4], cs[4]);  // arm joint 3 (X)
+  offset(4);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) st.w[i] = t[i];
+  rotate_axis(R, 1, sn[5], cs[5]);  // arm joint 4 (Y)
+  offset(5);
+  {  // arm joint 5 (Z) with the hand rotation folded into its angle
+    const T hs = armc<T>(right, m->hand_sc[0][0], m->hand_sc[1][0]);
+    const T hc = armc<T>(right, m->hand_sc[0][1], m->hand_sc[1][1]);
+    rotate_axis(R, 2, sn[6] * hc + cs[6] * hs, cs[6] * hc - sn[6] * hs);
+  }
+  T ht[3], d[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) ht[i] = armc<T>(right, m->hand_tH[0][i], m->hand_tH[1][i]);
+  matvec3(R, ht, d);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) st.h[i] = t[i] + d[i];
+  pose_error_aligned(R, st.h, RT1, tT1, st.e, tk, resync);
+  const T* e = st.e;
+  return e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3] + e[4] * e[4] + e[5] * e[5];
+}
+
+// u = J_a^-1 e_a, v = J_a^-1 c_a in closed form (see above); alpha = u.v,
+// beta = v.v.  An exactly singular block gives a zero inverse, as in
+// inv3_apply2.
+template <typename T, class SP>
+IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
+                                const T* sn, const T* cs, T* u, T* v, T& alpha, T& beta) {
+  const bool right = arm != 0;
+  const T* w = st.w;
+  const T* ev = st.e;
+  const T* ew = st.e + 3;
+  // linear rows moved from the hand point to w
+  T wh[3], cr[3], bl[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) wh[i] = w[i] - st.h[i];
+  cross3(ew, wh, cr);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) bl[i] = ev[i] + cr[i];
+  // G: P0 = w, P1 = w - p_1, P2 = w - o_2
+  T P1[3], P2[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    P1[i] = SP::zero_t(1, i) ? w[i] : w[i] - armc<T>(right, m->arm_t[0][1][i], m->arm_t[1][1][i]);
+    P2[i] = w[i] - st.o2[i];
+  }
+  const T det2 = P1[0] * P2[2] - P1[2] * P2[0];
+  const T dG = w[0] * det2;
+  const T rG = vsel<T>(dG != T(0), frcp(dG), T(0));
+  const T iP0 = det2 * rG, iD = w[0] * rG;
+  {
+    u[0] = bl[1] * iP0;
+    const T r0 = bl[0] + w[1] * u[0];
+    u[1] = -(P2[0] * r0 + P2[2] * bl[2]) * iD;
+    u[2] = (P1[2] * bl[2] + P1[0] * r0) * iD;
+  }
+  {  // root column at w: e_z x (w + (k, .)) = (-(w_y + k_y), w_x + k_x, 0)
+    v[0] = (w[0] + st.k[0]) * iP0;
+    const T r0 = w[1] * v[0] - (w[1] + st.k[1]);
+    v[1] = -P2[0] * r0 * iD;
+    v[2] = P1[0] * r0 * iD;
+  }
+  // H = Ry(q12) H''; slots 4, 5 = arm joints 3, 4
+  const T s3 = sn[4], c3 = cs[4], s4 = sn[5], c4 = cs[5];
+  const T rH = vsel<T>(c4 != T(0), frcp(c4), T(0));
+  const T c4r = c4 * rH;
+  const T c12 = st.c12, s12 = st.s12;
+  {  // e: z = Ry(q12)^T (e_w - (0, x1 + x2, x0))
+    const T z0 = ew[0], z1 = ew[1] - (u[1] + u[2]), z2 = ew[2] - u[0];
+    const T y0 = c12 * z0 - s12 * z2, y2 = s12 * z0 + c12 * z2;
+    u[5] = (c3 * y2 - s3 * z1) * rH;
+    u[4] = (c3 * z1 + s3 * y2) * c4r;
+    u[3] = y0 - s4 * u[5];
+  }
+  {  // root column: z = Ry(q12)^T (e_z - (0, v1 + v2, v0))
+    const T z1 = -(v[1] + v[2]), z2 = T(1) - v[0];
+    const T y0 = -s12 * z2, y2 = c12 * z2;
+    v[5] = (c3 * y2 - s3 * z1) * rH;
+    v[4] = (c3 * z1 + s3 * y2) * c4r;
+    v[3] = y0 - s4 * v[5];
+  }
+  alpha = T(0);
+  beta = T(0);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    alpha += u[k] * v[k];
+    beta += v[k] * v[k];
+  }
+}
+
 // lambda > 0: z_e, z_c = (J_a J_a^T + lambda I)^-1 [e_a, c_a]; alpha = c.z_e, beta = c.z_c.
 template <typename T>
 IKG_HD inline void arm_solve_damped(const T (&A)[6][8], T lambda, T* ze, T* zc, T& alpha, T& beta) {
@@ -1204,11 +1397,33 @@ IKG_HD inline void arm_dq_damped(const T (&A)[6][8], const T* ze, const T* zc, T
   }
 }
 
+// This lane's arm limits (pair layout), loaded once per solve when the
+// registers are available (IKG_LANE_LIMITS).
+template <typename T>
+struct ArmLimits {
+  T lo[kArmDof], hi[kArmDof];
+};
+template <typename T>
+IKG_HD inline void load_limits(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, ArmLimits<T>& L) {
+  const bool right = arm != 0;
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) {
+    L.lo[k] = armc<T>(right, m->arm_lo[0][k], m->arm_lo[1][k]);
+    L.hi[k] = armc<T>(right, m->arm_hi[0][k], m->arm_hi[1][k]);
+  }
+}
+
 // pin.integrate (q + dq * DT, :86) then projecttojointlimits (:89).
 template <typename T>
-IKG_HD inline void arm_update(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, T dt, T s, const T* dq, T& qc, T* qa) {
+IKG_HD inline void arm_update(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, T dt, T s, const T* dq, T& qc, T* qa,
+                              const ArmLimits<T>* lim = nullptr) {
   const bool right = arm != 0;
   qc = clampq(qc + s * dt, T(m->root_lo), T(m->root_hi));
+  if (lim) {
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) qa[k] = clampq(qa[k] + dq[k] * dt, lim->lo[k], lim->hi[k]);
+    return;
+  }
   if constexpr (is_packed<T>) {  // both arms in the lane: packed limits
 #pragma unroll
     for (int k = 0; k < kArmDof; ++k)

@@ -51,10 +51,23 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
   int it = 0;
   bool conv = false;
   T nrm[2];
+  ThetaTrack<T> tk[2] = {};
+  // the kernel's frame-1 path (kFrame1 models, lambda = 0) or the chest-frame one
+  const bool f1 = kFrame1<SP> && !damped;
   for (;;) {
     ArmState<T> st[2];
-    for (int arm = 0; arm < 2; ++arm)
-      nrm[arm] = arm_fk_error<T, SP>(&m, arm, sn[arm], cs[arm], RT[arm], tT[arm], st[arm]);
+    ArmStateF1<T> s1[2];
+    const bool resync = (it % Trig<T>::kResync) == 0;
+    ThetaTrack<T>* tkp[2] = {is_f64<T> ? &tk[0] : nullptr, is_f64<T> ? &tk[1] : nullptr};
+    for (int arm = 0; arm < 2; ++arm) {
+      if constexpr (kFrame1<SP>) {
+        if (f1) {
+          nrm[arm] = arm_fk_error_f1<T, SP>(&m, arm, sn[arm], cs[arm], RT[arm], tT[arm], s1[arm], tkp[arm], resync);
+          continue;
+        }
+      }
+      nrm[arm] = arm_fk_error<T, SP>(&m, arm, sn[arm], cs[arm], RT[arm], tT[arm], st[arm], nullptr, tkp[arm], resync);
+    }
     if (trace && it < trace_len) {
       trace[2 * it] = std::sqrt(nrm[0]);
       trace[2 * it + 1] = std::sqrt(nrm[1]);
@@ -83,6 +96,12 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
     for (int arm = 0; arm < 2; ++arm) {
       q_old[arm][0] = qc[arm];
       for (int k = 0; k < kArmDof; ++k) q_old[arm][k + 1] = qa[arm][k];
+      if constexpr (kFrame1<SP>) {
+        if (f1) {
+          arm_solve_f1<T, SP>(&m, arm, s1[arm], sn[arm], cs[arm], u[arm], v[arm], al[arm], be[arm]);
+          continue;
+        }
+      }
       if (damped) {
         arm_system(st[arm], A[arm]);
         arm_solve_damped(A[arm], prm.lambda, u[arm], v[arm], al[arm], be[arm]);
@@ -97,7 +116,9 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
         arm_dq_damped(A[arm], u[arm], v[arm], s, dq);
       else
         arm_dq(u[arm], v[arm], s, dq);
-      arm_update(&m, arm, prm.dt, s, dq, qc[arm], qa[arm]);
+      ArmLimits<T> lim;
+      load_limits(&m, arm, lim);
+      arm_update(&m, arm, prm.dt, s, dq, qc[arm], qa[arm], IKG_LANE_LIMITS ? &lim : nullptr);
       trig_advance(qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
     }
   }

@@ -60,8 +60,15 @@ __device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T
 // One 64-lane wave per workgroup holding `ppw` problems on lanes [0, 2 ppw).
 // A wave's issue cost does not depend on how many lanes are active, so small
 // batches are spread with ppw < 32 to occupy every SIMD.
+#ifndef IKG_WPE
+#define IKG_WPE 0
+#endif
 template <typename T, bool DAMPED, class SP>
-__global__ __launch_bounds__(64) void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
+__global__ __launch_bounds__(64)
+#if IKG_WPE
+__attribute__((amdgpu_waves_per_eu(1, IKG_WPE)))
+#endif
+void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             const T* __restrict__ targets,
                                                             const T* __restrict__ q0, int64_t q0_stride, int64_t B,
                                                             int64_t S, int ppw, T* __restrict__ q_out,

@@ -31,15 +31,42 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   bool conv = false;
   T x, xo;  // squared error norms of this lane's hand and the partner's
   ThetaTrack<T> tk{};
+#if IKG_LANE_LIMITS
+  ArmLimits<T> lim;
+  if constexpr (!is_packed<T>) load_limits(m, arm, lim);
+  const ArmLimits<T>* limp = is_packed<T> ? nullptr : &lim;
+#else
+  const ArmLimits<T>* limp = nullptr;
+#endif
+#ifdef IKG_PAD_OPS
+  // timing experiment: IKG_PAD_OPS independent fp64 FMAs per iteration (ILP 8)
+  T pad[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) pad[i] = qc + T(i);
+#endif
   for (;;) {
-    ArmState<T> st;
-    if constexpr (IKG_THETA_TRACK && is_f64<T>)  // fp32: atan2f is as cheap (measured)
-      x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, &tk, (it % Trig<T>::kResync) == 0);
-    else
-      x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
+#ifdef IKG_PAD_OPS
+#pragma unroll
+    for (int k = 0; k < IKG_PAD_OPS / 8; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pad[i] = pad[i] * T(0.999999) + T(1e-7);
+#endif
+    // fp32: atan2f is as cheap as the tracked angle (measured)
+    ThetaTrack<T>* tkp = (IKG_THETA_TRACK && is_f64<T>) ? &tk : nullptr;
+    const bool resync = (it % Trig<T>::kResync) == 0;
     // the step is formed before the stop test (discarded when the loop ends)
     // so the test's exchange/compare overlaps the solve instead of heading it
     T dq[6], alpha, beta, s;
+    if constexpr (kFrame1<SP> && !DAMPED) {
+      ArmStateF1<T> st;
+      x = arm_fk_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, tkp, resync);
+      T u[6], v[6];
+      arm_solve_f1<T, SP>(m, arm, st, sn, cs, u, v, alpha, beta);
+      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+      arm_dq(u, v, s, dq);
+    } else {
+    ArmState<T> st;
+    x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, tkp, resync);
     if constexpr (!DAMPED) {
       T u[6], v[6];
       arm_solve<T, SP>(st, u, v, alpha, beta);
@@ -52,6 +79,7 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
       s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
       arm_dq_damped(A, ze, zc, s, dq);
     }
+    }
     xo = pair_swap(x);
     if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
     if (both_below(x, xo, prm.eps2)) {  // |e_L| < eps and |e_R| < eps (:70)
@@ -62,10 +90,16 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     q_old[0] = qc;
 #pragma unroll
     for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
-    arm_update(m, arm, T(prm.dt), s, dq, qc, qa);
+    arm_update(m, arm, T(prm.dt), s, dq, qc, qa, limp);
     ++it;
     trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }
+#ifdef IKG_PAD_OPS
+  T ps = T(0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ps += pad[i];
+  if (any_of(ps == T(-12345.678))) it = -1;  // never true; keeps the padding live
+#endif
   it_out = it;
   nrm_out = sqrt(x);
   other_out = sqrt(xo);
