@@ -269,13 +269,14 @@ IKG_HD inline T fdiv(T a, T b) {
 #endif
 }
 
-// 1 / b (same refinement as fdiv, ~1 ulp)
+// 1 / b: v_rcp_f64 is good to ~2^-24 relative; one Newton step leaves <= 11
+// ulp and two give the correctly rounded reciprocal on every one of 2^20
+// log-uniform inputs (tools/ubench/rcp.hip, profiles/r02/ubench_rcp.txt)
 template <typename T>
 IKG_HD inline T frcp(T b) {
 #ifdef __HIP_DEVICE_COMPILE__
   if constexpr (is_f64<T>) {
     double r = __builtin_amdgcn_rcp(b);
-    r = fma(r, fma(-b, r, 1.0), r);
     r = fma(r, fma(-b, r, 1.0), r);
     return fma(r, fma(-b, r, 1.0), r);
   } else if constexpr (is_packed<T>) {
@@ -301,9 +302,8 @@ IKG_HD inline T fsqrt_unit(T x) {
     const double r = fma(-h, g, 0.5);
     g = fma(g, r, g);
     h = fma(h, r, h);
-    double d = fma(-g, g, x);
-    g = fma(d, h, g);
-    d = fma(-g, g, x);
+    // one correction already rounds correctly (tools/ubench/rcp.hip)
+    const double d = fma(-g, g, x);
     return fma(d, h, g);
   } else {
     return sqrt(x);
@@ -1031,6 +1031,58 @@ IKG_HD inline void trig_advance(T qc, const T* qa, const T* q_old, bool resync, 
   }
 }
 
+// Frame-1 trig slots (kFrame1 models): the sums the frame-1 FK consumes are
+// carried directly, so no angle additions run per update:
+//   0: q_root + q_0   1: q_0   2: q_1   3: q_1 + q_2   4: q_3   5: q_4
+//   6: q_5 + hand angle (the hand rotation about the same axis, fold_hand)
+template <typename T>
+IKG_HD inline void add_angles(T s1, T c1, T s2, T c2, T& s, T& c) {
+  s = s1 * c2 + c1 * s2;
+  c = c1 * c2 - s1 * s2;
+}
+
+template <typename T>
+IKG_HD inline void trig_exact_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, T qc, const T* qa, T* sn,
+                                 T* cs) {
+  T s[7], c[7];
+  trig_exact(qc, qa, s, c);
+  const bool right = arm != 0;
+  const T hs = armc<T>(right, m->hand_sc[0][0], m->hand_sc[1][0]);
+  const T hc = armc<T>(right, m->hand_sc[0][1], m->hand_sc[1][1]);
+  add_angles(s[0], c[0], s[1], c[1], sn[0], cs[0]);
+  sn[1] = s[1], cs[1] = c[1];
+  sn[2] = s[2], cs[2] = c[2];
+  add_angles(s[2], c[2], s[3], c[3], sn[3], cs[3]);
+  sn[4] = s[4], cs[4] = c[4];
+  sn[5] = s[5], cs[5] = c[5];
+  add_angles(s[6], c[6], hs, hc, sn[6], cs[6]);
+}
+
+template <typename T>
+IKG_HD inline void trig_advance_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, T qc, const T* qa,
+                                   const T* q_old, bool resync, T* sn, T* cs) {
+  T dj[7], d[7];
+  dj[0] = qc - q_old[0];
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) dj[k + 1] = qa[k] - q_old[k + 1];
+  d[0] = dj[0] + dj[1];
+  d[1] = dj[1];
+  d[2] = dj[2];
+  d[3] = dj[2] + dj[3];
+  d[4] = dj[4];
+  d[5] = dj[5];
+  d[6] = dj[6];
+  bool big = resync;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) big |= any_of(fabs(d[j]) > T(Trig<T>::kIncMax));
+  if (big) {
+    trig_exact_f1(m, arm, qc, qa, sn, cs);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
+  }
+}
+
 // FK + pose error; returns |e|^2 (inverse_geometry.py:58-67; the stop test
 // compares it with KParams::eps2).  WORLD = false
 // (the IK loop): everything in the chest frame (root_frame) -- the target is
@@ -1213,9 +1265,9 @@ IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__
                                 const T* RT, const T* tT, ArmStateF1<T>& st, ThetaTrack<T>* tk, bool resync) {
   static_assert(kFrame1<SP>, "frame-1 path needs the Nextage joint pattern");
   const bool right = arm != 0;
-  // frame 1 = chest Rz(q_root) at root_t, then arm joint 0 at p_0 with Rz(q_0)
-  const T sf = sn[0] * cs[1] + cs[0] * sn[1];
-  const T cf = cs[0] * cs[1] - sn[0] * sn[1];
+  // frame 1 = chest Rz(q_root) at root_t, then arm joint 0 at p_0 with Rz(q_0);
+  // trig slots as trig_exact_f1
+  const T sf = sn[0], cf = cs[0];
   T p0[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) p0[i] = SP::zero_t(0, i) ? T(0) : armc<T>(right, m->arm_t[0][0][i], m->arm_t[1][0][i]);
@@ -1249,9 +1301,10 @@ IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__
   offset(2);
 #pragma unroll
   for (int i = 0; i < 3; ++i) st.o2[i] = t[i];
-  rotate_axis(R, 1, sn[3], cs[3]);  // arm joint 2 (Y): R = Ry(q1 + q2)
-  st.c12 = R[0];
-  st.s12 = R[2];
+  // arm joint 2 (Y): R = Ry(q1 + q2) from its carried (sin, cos)
+  st.c12 = cs[3];
+  st.s12 = sn[3];
+  R[0] = st.c12, R[2] = st.s12, R[6] = -st.s12, R[8] = st.c12;
   offset(3);
   rotate_axis(R, 0, sn[4], cs[4]);  // arm joint 3 (X)
   offset(4);
@@ -1259,11 +1312,7 @@ IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__
   for (int i = 0; i < 3; ++i) st.w[i] = t[i];
   rotate_axis(R, 1, sn[5], cs[5]);  // arm joint 4 (Y)
   offset(5);
-  {  // arm joint 5 (Z) with the hand rotation folded into its angle
-    const T hs = armc<T>(right, m->hand_sc[0][0], m->hand_sc[1][0]);
-    const T hc = armc<T>(right, m->hand_sc[0][1], m->hand_sc[1][1]);
-    rotate_axis(R, 2, sn[6] * hc + cs[6] * hs, cs[6] * hc - sn[6] * hs);
-  }
+  rotate_axis(R, 2, sn[6], cs[6]);  // arm joint 5 (Z) + the hand rotation (slot 6)
   T ht[3], d[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) ht[i] = armc<T>(right, m->hand_tH[0][i], m->hand_tH[1][i]);

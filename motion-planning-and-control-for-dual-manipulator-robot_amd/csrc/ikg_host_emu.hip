@@ -46,7 +46,6 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
     for (int i = 0; i < 3; ++i) tT[arm][i] = tg[9 + i] + d[i];
     qc[arm] = qrow[m.root_q];
     for (int k = 0; k < kArmDof; ++k) qa[arm][k] = qrow[m.arm_q[arm][k]];
-    trig_exact(qc[arm], qa[arm], sn[arm], cs[arm]);
   }
   int it = 0;
   bool conv = false;
@@ -54,6 +53,12 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
   ThetaTrack<T> tk[2] = {};
   // the kernel's frame-1 path (kFrame1 models, lambda = 0) or the chest-frame one
   const bool f1 = kFrame1<SP> && !damped;
+  for (int arm = 0; arm < 2; ++arm) {
+    if (f1)
+      trig_exact_f1(&m, arm, qc[arm], qa[arm], sn[arm], cs[arm]);
+    else
+      trig_exact(qc[arm], qa[arm], sn[arm], cs[arm]);
+  }
   for (;;) {
     ArmState<T> st[2];
     ArmStateF1<T> s1[2];
@@ -119,7 +124,10 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
       ArmLimits<T> lim;
       load_limits(&m, arm, lim);
       arm_update(&m, arm, prm.dt, s, dq, qc[arm], qa[arm], IKG_LANE_LIMITS ? &lim : nullptr);
-      trig_advance(qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
+      if (f1)
+        trig_advance_f1(&m, arm, qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
+      else
+        trig_advance(qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
     }
   }
   for (int j = 0; j < m.nq; ++j) qo[j] = qrow[j];

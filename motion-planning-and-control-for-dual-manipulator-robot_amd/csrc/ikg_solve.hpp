@@ -25,8 +25,12 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
                                   const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
                                   T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out) {
   static_assert(!(DAMPED && is_packed<T>), "the packed layout implements lambda = 0 only");
+  constexpr bool F1 = kFrame1<SP> && !DAMPED;  // frame-1 path, its own trig slots
   T sn[7], cs[7];
-  trig_exact(qc, qa, sn, cs);
+  if constexpr (F1)
+    trig_exact_f1(m, arm, qc, qa, sn, cs);
+  else
+    trig_exact(qc, qa, sn, cs);
   int it = 0;
   bool conv = false;
   T x, xo;  // squared error norms of this lane's hand and the partner's
@@ -57,7 +61,7 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     // the step is formed before the stop test (discarded when the loop ends)
     // so the test's exchange/compare overlaps the solve instead of heading it
     T dq[6], alpha, beta, s;
-    if constexpr (kFrame1<SP> && !DAMPED) {
+    if constexpr (F1) {
       ArmStateF1<T> st;
       x = arm_fk_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, tkp, resync);
       T u[6], v[6];
@@ -92,7 +96,10 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
     arm_update(m, arm, T(prm.dt), s, dq, qc, qa, limp);
     ++it;
-    trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
+    if constexpr (F1)
+      trig_advance_f1(m, arm, qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
+    else
+      trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }
 #ifdef IKG_PAD_OPS
   T ps = T(0);
