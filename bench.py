@@ -186,6 +186,19 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
+        # executed FP ops per problem-iteration of this kernel (rocprofv3 FMA/MUL/ADD/TRANS counters,
+        # tools/pmc_flops.py): the frame-1 loop does ~1/3 of the reference formulation's 3,144, so the
+        # SURVEY-count frac above overstates hardware use; executed_frac is the hardware VALU fraction
+        executed = None
+        fl = os.path.join(ROOT, "profiles", f"flops_{args.dtype}_b{B}.json")
+        if os.path.exists(fl) and kname == "ikg_pair_batch_kernel" and sum_iters:
+            with open(fl) as f:
+                per_it = json.load(f)["fp_ops_per_problem_iter"]
+            ex = sum_iters * per_it / (kern_ms * 1e-3) / 1e12
+            waves = -(-B // 32)
+            executed = {"fp_ops_per_problem_iter": per_it, "achieved": ex, "frac": ex / PEAK_VALU[args.dtype],
+                        "unit": "TFLOP/s", "waves": waves, "simds": cus * 4,
+                        "source": os.path.relpath(fl, ROOT)}
         out = {
             "metric": METRIC, "value": value, "unit": "converged solves/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_step * 1e3,
@@ -211,6 +224,7 @@ def main():
                 "kernel": kname + (" + ikg_collide_continue_kernel" if args.collision else ""),
                 "kernel_ms": kern_ms,
                 "work": f"sum(iters)={sum_iters} x {F_ITER} FP ops (SURVEY §8a)",
+                "executed": executed,
             },
             "roofline_hbm": {
                 "bound": "hbm", "achieved": abytes / (kern_ms * 1e-3) / 1e9, "peak": PEAK_HBM, "unit": "GB/s",

@@ -1,5 +1,5 @@
 """Run one IK configuration `reps` times (for rocprofv3 --pmc passes).
-usage: pmc_probe.py B dtype ppw reps"""
+usage: pmc_probe.py B dtype ppw reps [--save-iters path.npy]"""
 import os
 import sys
 
@@ -26,3 +26,6 @@ for _ in range(reps):
     s.solve_into(tg, q0, qo, cv, it, er, code, st, ppw=ppw)
 torch.cuda.synchronize()
 print("sum iters", int(it.to(torch.int64).sum()), "converged", int(cv.sum()))
+if "--save-iters" in sys.argv:
+    import numpy as np
+    np.save(sys.argv[sys.argv.index("--save-iters") + 1], it.cpu().numpy())

@@ -5,7 +5,7 @@
 # copies the judged files into profiles/<round>/.
 ROOT=$(pwd); O=$ROOT/gpurun_out/refresh; mkdir -p $O; export TMPDIR=/tmp
 fatal() { case $1 in 0|1) return 0;; *) echo "FATAL $2 rc=$1" | tee -a $O/summary.txt; exit $1;; esac; }
-timeout -k 10 900 python -m pytest tests -m gpu -q > $O/pytest_gpu.log 2>&1; fatal $? pytest
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1; fatal $? pytest
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1; fatal $? smoke
 timeout -k 10 300 python bench.py > $O/bench_b4096_f64.json 2> $O/bench.err; fatal $? bench
 timeout -k 10 300 python bench.py --dtype f32 --batch 65536 --no-cpu-baseline > $O/bench_b65536_f32.json 2>> $O/bench.err; fatal $? bench32
