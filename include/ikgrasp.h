@@ -55,11 +55,14 @@ enum ikg_status {
 
 /* kernel variant selector (ikg_params.variant) */
 enum ikg_variant {
-  IKG_VARIANT_AUTO = 0,   /* ikg_solve_batch: PACKED where it applies and B > 4 pair waves per CU,
-                             else PAIR; ikg_solve_multistart: PAIR */
+  IKG_VARIANT_AUTO = 0,   /* ikg_solve_batch: QUAD where it applies and B <= 8,192 (the batch
+                             leaves SIMDs idle), PACKED where it applies and B > 4 pair waves
+                             per CU, else PAIR; ikg_solve_multistart: PAIR */
   IKG_VARIANT_PAIR = 1,   /* two lanes per problem (one arm per lane), 32 problems / wave */
-  IKG_VARIANT_PACKED = 2  /* fp32, Nextage-class models, lambda = 0: one lane per problem with
+  IKG_VARIANT_PACKED = 2, /* fp32, Nextage-class models, lambda = 0: one lane per problem with
                              both arms packed in 2-vectors (v_pk_*_f32), 64 problems / wave */
+  IKG_VARIANT_QUAD = 3    /* Nextage-class models, lambda = 0: four lanes per arm (rows of the
+                             kinematic chain split over them), 8 problems / wave */
 };
 
 /* Robot + grasp-object description (produced by the model compiler,

@@ -181,7 +181,8 @@ int check_params(const ikg_params* p) {
   if (!std::isfinite(p->dt)) return fail(IKG_EINVAL, "dt must be finite");
   if (p->max_iters < 0) return fail(IKG_EINVAL, "max_iters must be >= 0");
   if (!(p->lambda >= 0) || !std::isfinite(p->lambda)) return fail(IKG_EINVAL, "lambda must be >= 0");
-  if (p->variant != IKG_VARIANT_AUTO && p->variant != IKG_VARIANT_PAIR && p->variant != IKG_VARIANT_PACKED)
+  if (p->variant != IKG_VARIANT_AUTO && p->variant != IKG_VARIANT_PAIR && p->variant != IKG_VARIANT_PACKED &&
+      p->variant != IKG_VARIANT_QUAD)
     return fail(IKG_EINVAL, "variant %d not available in this build", p->variant);
   if (p->problems_per_wave < 0 || p->problems_per_wave > 32)
     return fail(IKG_EINVAL, "problems_per_wave must be in [0, 32]");
@@ -209,6 +210,8 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   a.variant = params->variant;
   if (params->variant == IKG_VARIANT_PACKED && (sizeof(T) != 4 || model->spec != ikg::kSpecNextage || params->lambda > 0))
     return fail(IKG_EINVAL, "variant PACKED needs fp32, a Nextage-class model and lambda = 0");
+  if (params->variant == IKG_VARIANT_QUAD && (model->spec != ikg::kSpecNextage || params->lambda > 0))
+    return fail(IKG_EINVAL, "variant QUAD needs a Nextage-class model and lambda = 0");
   Staging st(s);
   const bool host = flags & IKG_FLAG_HOST_POINTERS;
   if (host) {
@@ -258,6 +261,8 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   a.variant = params->variant;
   if (params->variant == IKG_VARIANT_PACKED && (sizeof(T) != 4 || model->spec != ikg::kSpecNextage || params->lambda > 0))
     return fail(IKG_EINVAL, "variant PACKED needs fp32, a Nextage-class model and lambda = 0");
+  if (params->variant == IKG_VARIANT_QUAD && (model->spec != ikg::kSpecNextage || params->lambda > 0))
+    return fail(IKG_EINVAL, "variant QUAD needs a Nextage-class model and lambda = 0");
   if (params->check_collision) {
     const ikg::KCollision<T>* dc = nullptr;
     if ((rc = model->collision_tables<T>(device, &dc))) return rc;

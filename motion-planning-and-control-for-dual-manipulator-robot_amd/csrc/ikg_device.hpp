@@ -320,7 +320,8 @@ IKG_HD inline T fsqrt_unit(T x) {
 // Exchange a value with the partner lane (lane ^ 1) through a DPP quad_perm
 // [1,0,3,2]: no LDS traffic, one VALU op per dword.
 __device__ inline int pair_swap_i32(int x) {
-  return __builtin_amdgcn_update_dpp(x, x, 0xB1, 0xF, 0xF, false);
+  // every lane is written: mov_dpp needs no "old" operand (and no copy of x)
+  return __builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
 }
 __device__ inline float pair_swap(float x) {
   return __int_as_float(pair_swap_i32(__float_as_int(x)));
@@ -1075,12 +1076,11 @@ IKG_HD inline void trig_advance_f1(const KModel<typename LaneT<T>::E>* __restric
   bool big = resync;
 #pragma unroll
   for (int j = 0; j < 7; ++j) big |= any_of(fabs(d[j]) > T(Trig<T>::kIncMax));
-  if (big) {
-    trig_exact_f1(m, arm, qc, qa, sn, cs);
-  } else {
+  // the step always runs in place and the (rare) exact path overwrites it: the
+  // common path then needs no register copies to merge the two
 #pragma unroll
-    for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
-  }
+  for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
+  if (big) trig_exact_f1(m, arm, qc, qa, sn, cs);
 }
 
 // FK + pose error; returns |e|^2 (inverse_geometry.py:58-67; the stop test

@@ -31,32 +31,6 @@
 namespace ikg {
 
 
-template <typename T>
-__device__ inline void load_q(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow, T& qc, T* qa) {
-  qc = qrow[m->root_q];
-  const bool right = arm != 0;
-#pragma unroll
-  for (int k = 0; k < kArmDof; ++k) qa[k] = qrow[right ? m->arm_q[1][k] : m->arm_q[0][k]];
-}
-
-template <typename T>
-__device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow, int it, T qc,
-                               const T* qa, T* __restrict__ qo) {
-  const bool right = arm != 0;
-  if (!right) {
-    qo[m->root_q] = qc;
-    // passive joints (HEAD_JOINT0/1): zero Jacobian columns, so only the clamp
-    // of the first update moves them (tools.py:21-22)
-    for (int i = 0; i < m->n_passive; ++i) {
-      const int j = m->passive_q[i];
-      const T v = qrow[j];
-      qo[j] = it > 0 ? clampq(v, m->lo[j], m->hi[j]) : v;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kArmDof; ++k) qo[right ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
-}
-
 // One 64-lane wave per workgroup holding `ppw` problems on lanes [0, 2 ppw).
 // A wave's issue cost does not depend on how many lanes are active, so small
 // batches are spread with ppw < 32 to occupy every SIMD.
@@ -274,10 +248,31 @@ static int64_t packed_min_batch() {
   return v;
 }
 
+// The quad layout (ikg_quad.hip, 8 lanes and ~2/3 of the pair layout's
+// instructions per problem-update, 1/4 of the problems per wave) wins while the
+// batch leaves SIMDs idle; AUTO takes it up to quad_max_batch().
+template <typename T>
+bool quad_applies(const KParams<T>& prm, int spec) {
+  return spec == kSpecNextage && !(prm.lambda > T(0));
+}
+
+static int64_t quad_max_batch() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("IKG_QUAD_MAX_BATCH");
+    v = e ? atol(e) : 0;  // measured no faster than PAIR: explicit variant only
+  }
+  return (int64_t)v;
+}
+
 template <typename T>
 hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,
                              hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
+  if (a.variant == IKG_VARIANT_QUAD || (a.variant == IKG_VARIANT_AUTO && a.B <= quad_max_batch())) {
+    if (quad_applies(prm, spec)) return launch_quad_batch<T>(dmodel, prm, a, s);
+    if (a.variant == IKG_VARIANT_QUAD) return hipErrorInvalidValue;  // checked by the C-ABI first
+  }
   if constexpr (std::is_same<T, float>::value) {
     const bool want = a.variant == IKG_VARIANT_PACKED || (a.variant == IKG_VARIANT_AUTO && a.B >= packed_min_batch());
     if (want && packed_applies(prm, spec)) {

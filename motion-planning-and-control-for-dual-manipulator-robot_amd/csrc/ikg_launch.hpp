@@ -59,6 +59,10 @@ hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, con
 hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>& prm, const BatchArgs& a,
                                hipStream_t s);
 
+// quad layout (8 lanes per problem), Nextage specialisation (ikg_quad.hip)
+template <typename T>
+hipError_t launch_quad_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s);
+
 template <typename T>
 hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, const MultiArgs& a, int spec,
                              hipStream_t s);

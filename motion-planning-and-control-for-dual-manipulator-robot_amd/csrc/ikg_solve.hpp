@@ -6,6 +6,34 @@
 
 namespace ikg {
 
+// q row -> this arm's (root, arm joints) and back (pair and quad layouts)
+template <typename T>
+__device__ inline void load_q(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow, T& qc, T* qa) {
+  qc = qrow[m->root_q];
+  const bool right = arm != 0;
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) qa[k] = qrow[right ? m->arm_q[1][k] : m->arm_q[0][k]];
+}
+
+template <typename T>
+__device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T* __restrict__ qrow, int it, T qc,
+                               const T* qa, T* __restrict__ qo) {
+  const bool right = arm != 0;
+  if (!right) {
+    qo[m->root_q] = qc;
+    // passive joints (HEAD_JOINT0/1): zero Jacobian columns, so only the clamp
+    // of the first update moves them (tools.py:21-22)
+    for (int i = 0; i < m->n_passive; ++i) {
+      const int j = m->passive_q[i];
+      const T v = qrow[j];
+      qo[j] = it > 0 ? clampq(v, m->lo[j], m->hi[j]) : v;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kArmDof; ++k) qo[right ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
+}
+
+
 // Stop test of inverse_geometry.py:70 on squared norms (KParams::eps2):
 // pair layout = this lane's hand and the partner's; packed = both halves.
 template <typename T, typename E>

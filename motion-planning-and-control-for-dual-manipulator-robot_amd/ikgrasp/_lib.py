@@ -16,7 +16,7 @@ IKG_MAX_PAIRS = 1024
 IKG_ARM_DOF = 6
 IKG_F64, IKG_F32 = 0, 1
 IKG_FLAG_HOST_POINTERS = 1
-IKG_VARIANT_AUTO, IKG_VARIANT_PAIR, IKG_VARIANT_PACKED = 0, 1, 2
+IKG_VARIANT_AUTO, IKG_VARIANT_PAIR, IKG_VARIANT_PACKED, IKG_VARIANT_QUAD = 0, 1, 2, 3
 # pinocchio.ReferenceFrame values (ikg_reference_frame)
 IKG_WORLD, IKG_LOCAL, IKG_LOCAL_WORLD_ALIGNED = 0, 1, 2
 

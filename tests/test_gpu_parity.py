@@ -300,8 +300,48 @@ def test_problems_per_wave_does_not_change_results(solver):
         assert np.array_equal(s.q, ref.q) and np.array_equal(s.iters, ref.iters) and np.array_equal(s.err, ref.err)
 
 
+# ---------------------------------------------------------------- quad layout (IKG_VARIANT_QUAD)
+def test_fixture_parity_fp64_quad_layout(solver, oracle_cases):
+    """The quad layout (8 lanes per problem, ikg_quad.hip) against the fixtures
+    with the fp64 gates of test_fixture_parity_fp64."""
+    c = oracle_cases
+    sol = solver.solve(c["targets"], c["q0"], dtype="f64", variant=3)
+    assert np.array_equal(sol.converged, c["converged"])
+    assert np.array_equal(sol.iters, c["iters"])
+    conv = c["converged"]
+    assert np.abs(sol.q[conv] - c["q"][conv]).max() <= 1e-9
+    assert np.abs(sol.err[conv] - c["err"][conv]).max() <= 1e-10
+
+
+def test_quad_layout_matches_pair_layout(solver, kat):
+    """Same frame-1 arithmetic in another lane layout: identical flags and update
+    counts, q to rounding (fp64), at the headline batch size; KATs within 1e-12."""
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(4096, seed=0)
+    a = solver.solve(tg, np.zeros(15), dtype="f64", variant=1)
+    b = solver.solve(tg, np.zeros(15), dtype="f64", variant=3)
+    assert np.array_equal(a.converged, b.converged) and np.array_equal(a.iters, b.iters)
+    assert np.abs(a.q - b.q).max() <= 1e-9
+    kt = np.stack([_placement_row(kat["cube_placement"]), _placement_row(kat["cube_placement_target"])])
+    k = solver.solve(kt, np.zeros(15), dtype="f64", variant=3)
+    assert k.iters.tolist() == [740, 736]
+    assert np.abs(k.q[0] - np.array(kat["q0"])).max() <= 1e-12
+    assert np.abs(k.q[1] - np.array(kat["qe"])).max() <= 1e-12
+    # ragged batches: the last wave holds 1..7 problems
+    for B in (1, 3, 9, 15):
+        p = solver.solve(tg[-B:], np.zeros(15), dtype="f64", variant=3)
+        assert np.array_equal(p.q, b.q[-B:]) and np.array_equal(p.iters, b.iters[-B:])
+
+
+def test_quad_variant_rejected_for_damped_solves(solver, kat):
+    from ikgrasp._lib import IkgError
+    tg = np.stack([_placement_row(kat["cube_placement"])])
+    with pytest.raises(IkgError):
+        solver.solve(tg, np.zeros(15), dtype="f64", variant=3, lam=1e-3)
+
+
 # ---------------------------------------------------------------- packed fp32 layout (IKG_VARIANT_PACKED)
-@pytest.mark.parametrize("variant", [1, 2])  # PAIR, PACKED
+@pytest.mark.parametrize("variant", [1, 2, 3])  # PAIR, PACKED, QUAD
 def test_fixture_parity_fp32_layouts(solver, oracle_cases, variant):
     c = oracle_cases
     sol = solver.solve(c["targets"], c["q0"], dtype="f32", variant=variant)
