@@ -260,7 +260,7 @@ static int64_t quad_max_batch() {
   static long v = -1;
   if (v < 0) {
     const char* e = getenv("IKG_QUAD_MAX_BATCH");
-    v = e ? atol(e) : 0;  // measured no faster than PAIR (DESIGN.md §3e): explicit variant only
+    v = e ? atol(e) : 0;  // measured no faster than PAIR (DESIGN.md §3a.2): explicit variant only
   }
   return (int64_t)v;
 }

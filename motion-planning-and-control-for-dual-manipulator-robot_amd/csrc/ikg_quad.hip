@@ -16,7 +16,7 @@
 //     waits on another except at the broadcasts and the arm exchange.
 // Per lane and update that is ~290 fp64 operations and ~70 32-bit DPP moves
 // against ~405 fp64 operations for the pair layout's one lane per arm
-// (DESIGN.md §3e).  Same device functions as the frame-1 pair path
+// (DESIGN.md §3a.2).  Same device functions as the frame-1 pair path
 // (ikg_device.hpp: log6_iter, arm_solve_f1, arm_update, Trig<T>::step), so the
 // iterates agree with it to rounding.
 #include <hip/hip_runtime.h>
