@@ -720,6 +720,46 @@ __device__ __forceinline__ void cont_update(const KModel<T>* __restrict__ m, con
   trig_advance(qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);
 }
 
+// Certified-stretch updates (no collision check ahead, so no joint frames):
+// the batch kernel's frame-1 loop for kFrame1 models with lambda = 0 (trig
+// slots of trig_exact_f1), else the chest-frame loop of cont_step.
+template <class SP, bool DAMPED>
+constexpr bool kStretchF1 = kFrame1<SP> && !DAMPED;
+
+template <typename T, bool DAMPED, class SP>
+__device__ __forceinline__ T stretch_step(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm,
+                                          const T* sn, const T* cs, const T* RT, const T* tT, T* dq, T& s,
+                                          ThetaTrack<T>* tk, bool resync) {
+  if constexpr (kStretchF1<SP, DAMPED>) {
+    ArmStateF1<T> st;
+    const T x = arm_fk_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, (IKG_THETA_TRACK && is_f64<T>) ? tk : nullptr,
+                                       resync);
+    T u[6], v[6], alpha, beta;
+    arm_solve_f1<T, SP>(m, arm, st, sn, cs, u, v, alpha, beta);
+    s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
+    arm_dq(u, v, s, dq);
+    return x;
+  } else {
+    return cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, tk, resync);
+  }
+}
+
+template <typename T, bool DAMPED, class SP>
+__device__ __forceinline__ void stretch_update(const KModel<T>* __restrict__ m, const KParams<T>& prm, int arm, T s,
+                                               const T* dq, int it, T& qc, T* qa, T* sn, T* cs,
+                                               const ArmLimits<T>& lim) {
+  if constexpr (kStretchF1<SP, DAMPED>) {
+    T q_old[7];
+    q_old[0] = qc;
+#pragma unroll
+    for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
+    arm_update(m, arm, prm.dt, s, dq, qc, qa, &lim);
+    trig_advance_f1(m, arm, qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);
+  } else {
+    cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
+  }
+}
+
 // In-kernel certified stretch (IK lanes of the continuation).  The wave's
 // problems leave together, as soon as one of them needs the main loop (a
 // check, or max_iters): a problem left waiting while the others finish their
@@ -757,11 +797,14 @@ __device__ __noinline__ void cert_stretch(const KModel<T>* __restrict__ m, int m
   T qc = qc_io;
   int it = it_io;
   ThetaTrack<T> tk{};
+  ArmLimits<T> lim;
+  load_limits(m, arm, lim);
+  if constexpr (kStretchF1<SP, DAMPED>) trig_exact_f1(m, arm, qc, qa, sn, cs);  // frame-1 slots (a resync)
   for (int n = 0;; ++n) {
     if (__any(it >= max_iters)) break;
     T dq[6], s;
-    const T x = cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, &tk,
-                                                n == 0 || (it % Trig<T>::kResync) == 0);
+    const T x = stretch_step<T, DAMPED, SP>(m, prm, arm, sn, cs, RT, tT, dq, s, &tk,
+                                            n == 0 || (it % Trig<T>::kResync) == 0);
     const T xo = pair_swap(x);
     const T em = motion_bound(qc, qa, qcert, Rr);
     const T et = em + pair_swap(em);
@@ -769,9 +812,11 @@ __device__ __noinline__ void cert_stretch(const KModel<T>* __restrict__ m, int m
     if (__any(conv2 && !(et < cbudget))) break;
     if (conv2 && li == 0) SKIP_STAT(1, 1);
     if (li == 0) SKIP_STAT(6, 1);
-    cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
+    stretch_update<T, DAMPED, SP>(m, prm, arm, s, dq, it, qc, qa, sn, cs, lim);
     ++it;
   }
+  // the caller's loop reads the chest-frame slots
+  if constexpr (kStretchF1<SP, DAMPED>) trig_exact(qc, qa, sn, cs);
   qc_io = qc;
   it_io = it;
 #pragma unroll
@@ -1085,7 +1130,12 @@ __global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* _
     qc = qrow[m->root_q];
 #pragma unroll
     for (int k = 0; k < kArmDof; ++k) qa[k] = qrow[arm ? m->arm_q[1][k] : m->arm_q[0][k]];
-    trig_exact(qc, qa, sn, cs);
+    if constexpr (kStretchF1<SP, DAMPED>)
+      trig_exact_f1(m, arm, qc, qa, sn, cs);
+    else
+      trig_exact(qc, qa, sn, cs);
+    ArmLimits<T> lim;
+    load_limits(m, arm, lim);
     const T budget = stretch_rec[p * kStretchRec];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
@@ -1098,8 +1148,8 @@ __global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* _
     ThetaTrack<T> tk{};
     for (int r = 0;; ++r) {
       T dq[6], s;
-      x = cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, &tk,
-                                          r == 0 || (it % Trig<T>::kResync) == 0);
+      x = stretch_step<T, DAMPED, SP>(m, prm, arm, sn, cs, RT, tT, dq, s, &tk,
+                                      r == 0 || (it % Trig<T>::kResync) == 0);
       const T xo = pair_swap(x);
       const T em = motion_bound(qc, qa, qcert, Rr);
       const T et = em + pair_swap(em);
@@ -1111,7 +1161,7 @@ __global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* _
         if (!(et < budget)) break;
         if (arm == 0) SKIP_STAT(1, 1);
       }
-      cont_update(m, prm, arm, s, dq, it, qc, qa, sn, cs);
+      stretch_update<T, DAMPED, SP>(m, prm, arm, s, dq, it, qc, qa, sn, cs, lim);
       ++it;
     }
     if (!writer) continue;
