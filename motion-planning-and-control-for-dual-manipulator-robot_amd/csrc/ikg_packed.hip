@@ -5,6 +5,9 @@
 // at B = 131,072, tools/ablate.py).
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <cstdlib>
+
 #include "ikg_device.hpp"
 #include "ikg_launch.hpp"
 #include "ikg_solve.hpp"
@@ -15,7 +18,14 @@ namespace ikg {
 // Packed fp32 layout: one lane per problem, both arms in 2-vectors, so every
 // v_pk_{fma,mul,add}_f32 advances both arms and a wave holds 64 problems
 // (DESIGN.md §3).  Same loop, same arithmetic as the pair kernel's fp32 path.
-template <class SP>
+//
+// ONE_WAVE: the kernel claims all 256 AGPRs (an empty asm clobber), so the
+// hardware fits one wave per SIMD.  A launch of at most one wave per SIMD then
+// cannot be dispatched with two waves sharing a SIMD while another idles --
+// which the dispatcher does after some kernels (after the collision
+// continuation, 19-46 of 1,024 SIMDs held two waves of the next 1,024-wave
+// launch and the kernel took 2.2 ms instead of 1.4; tools/placement_probe.py).
+template <class SP, bool ONE_WAVE>
 __global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               KParams<float> prm, const float* __restrict__ targets,
                                                               const float* __restrict__ q0, int64_t q0_stride,
@@ -23,6 +33,7 @@ __global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float
                                                               uint8_t* __restrict__ conv_out,
                                                               int32_t* __restrict__ iters_out,
                                                               float* __restrict__ err_out) {
+  if constexpr (ONE_WAVE) asm volatile("" ::: "a255");
   const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (p >= B) return;
   const int64_t tgt = S > 1 ? p / S : p;
@@ -57,12 +68,44 @@ __global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float
   }
 }
 
+// Experiment knob (tools/dvfs_probe.py): dynamic LDS reserved per single-wave
+// workgroup, which caps how many workgroups the dispatcher may put on one CU.
+static size_t packed_lds_pad() {
+  static long v = -1;
+  if (v < 0) {
+    const char* e = getenv("IKG_PACKED_LDS_PAD");
+    v = e ? atol(e) : 0;
+  }
+  return (size_t)v;
+}
+
+// SIMDs of the current device (4 per CU), cached per device
+static unsigned simd_count() {
+  constexpr int kDevs = 64;
+  static std::atomic<unsigned> cache[kDevs];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDevs) return 1024;
+  unsigned v = cache[dev].load(std::memory_order_relaxed);
+  if (v) return v;
+  int cus = 256;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  v = 4u * (unsigned)cus;
+  cache[dev].store(v, std::memory_order_relaxed);
+  return v;
+}
+
 hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>& prm, const BatchArgs& a,
                                hipStream_t s) {
   const dim3 grid((unsigned)((a.B + 63) / 64));
-  hipLaunchKernelGGL((ikg_packed_batch_kernel<SpecNextage>), grid, dim3(64), 0, s, dmodel, prm,
-                     (const float*)a.targets, (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out,
-                     a.converged, a.iters, (float*)a.err_out);
+  if (grid.x <= simd_count()) {
+    hipLaunchKernelGGL((ikg_packed_batch_kernel<SpecNextage, true>), grid, dim3(64), packed_lds_pad(), s, dmodel, prm,
+                       (const float*)a.targets, (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out,
+                       a.converged, a.iters, (float*)a.err_out);
+  } else {
+    hipLaunchKernelGGL((ikg_packed_batch_kernel<SpecNextage, false>), grid, dim3(64), packed_lds_pad(), s, dmodel,
+                       prm, (const float*)a.targets, (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out,
+                       a.converged, a.iters, (float*)a.err_out);
+  }
   return hipGetLastError();
 }
 
