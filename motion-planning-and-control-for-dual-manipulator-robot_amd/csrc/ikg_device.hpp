@@ -30,6 +30,11 @@
 #ifndef IKG_TAYLOR_MUL
 #define IKG_TAYLOR_MUL 1
 #endif
+// fp64 log6 in the loop: Pinocchio's small-angle series for alpha, beta below
+// precision<3>() (1) or the closed forms throughout (0)
+#ifndef IKG_LOG6_SERIES
+#define IKG_LOG6_SERIES 1
+#endif
 // pair kernel: per-lane joint limits held in registers (12 fp64) instead of
 // clamping against both arms' scalar limits and selecting
 #ifndef IKG_LANE_LIMITS
@@ -608,6 +613,7 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
   }
   T beta;
   if constexpr (is_f64<T>) {
+#if IKG_LOG6_SERIES
 #if IKG_TAYLOR_MUL
     // Pinocchio's series terms t2/12, t2^2/720 as products with the rounded
     // reciprocals (<= 1 ulp of each term; the branch serves theta < 1.2e-4):
@@ -620,6 +626,13 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
 #endif
     beta = vsel<T>(below, bs, (T(1) - alpha) * inv_t2);
     alpha = vsel<T>(below, as, alpha);
+#else
+    // no series branch: theta (1 + cos)/(2 sin) has no cancellation at small
+    // theta, and (1 - alpha)/theta^2's cancellation error (eps/theta^2) reaches
+    // v only through beta (w.p) w with |w|^2 = theta^2: ~eps |p| absolute
+    (void)below;
+    beta = (T(1) - alpha) * inv_t2;
+#endif
   } else {
     const T as = T(1) - t2 * (T(1.f / 12) + t2 * (T(1.f / 720) + t2 * T(1.f / 30240)));
     const T bs = T(1.f / 12) + t2 * (T(1.f / 720) + t2 * (T(1.f / 30240) + t2 * T(1.f / 1209600)));
@@ -653,7 +666,25 @@ struct Trig<double> {
   // |d| <= 0.025: the dropped terms d^9/9! and d^8/8! are < 1e-18 relative.
   // Measured steps (uniform sampler, oracle): max 0.0212, 99.99% < 0.02.
   static constexpr double kIncMax = 0.025;
+  // |d| <= 0.25 for step_med: the first dropped terms d^15/15!, d^16/16! < 1e-21
+  static constexpr double kIncMed = 0.25;
   static constexpr int kResync = IKG_RESYNC64;
+  IKG_HD static inline void step_med(double d, double& s, double& c) {
+    const double d2 = d * d;
+    const double sd =
+        d + d * d2 *
+                (-1.0 / 6 +
+                 d2 * (1.0 / 120 +
+                       d2 * (-1.0 / 5040 + d2 * (1.0 / 362880 + d2 * (-1.0 / 39916800 + d2 * (1.0 / 6227020800.0))))));
+    const double cd =
+        1.0 + d2 * (-0.5 + d2 * (1.0 / 24 +
+                                 d2 * (-1.0 / 720 +
+                                       d2 * (1.0 / 40320 + d2 * (-1.0 / 3628800 +
+                                                                 d2 * (1.0 / 479001600 + d2 * (-1.0 / 87178291200.0)))))));
+    const double sn = s * cd + c * sd;
+    c = c * cd - s * sd;
+    s = sn;
+  }
   IKG_HD static inline void step(double d, double& s, double& c) {
     const double d2 = d * d;
     const double sd = d + d * d2 * (-1.0 / 6 + d2 * (1.0 / 120 + d2 * (-1.0 / 5040)));
@@ -666,7 +697,16 @@ struct Trig<double> {
 template <>
 struct Trig<float> {
   static constexpr float kIncMax = 0.1f;
+  static constexpr float kIncMed = 0.5f;  // d^11/11!, d^12/12! < 2e-11 for step_med
   static constexpr int kResync = 16;
+  IKG_HD static inline void step_med(float d, float& s, float& c) {
+    const float d2 = d * d;
+    const float sd = d + d * d2 * (-1.0f / 6 + d2 * (1.0f / 120 + d2 * (-1.0f / 5040 + d2 * (1.0f / 362880))));
+    const float cd = 1.0f + d2 * (-0.5f + d2 * (1.0f / 24 + d2 * (-1.0f / 720 + d2 * (1.0f / 40320 + d2 * (-1.0f / 3628800)))));
+    const float sn = s * cd + c * sd;
+    c = c * cd - s * sd;
+    s = sn;
+  }
   IKG_HD static inline void step(float d, float& s, float& c) {
     const float d2 = d * d;
     const float sd = d + d * d2 * (-1.0f / 6 + d2 * (1.0f / 120 + d2 * (-1.0f / 5040)));
@@ -679,7 +719,16 @@ struct Trig<float> {
 template <>
 struct Trig<v2f> {
   static constexpr float kIncMax = Trig<float>::kIncMax;
+  static constexpr float kIncMed = Trig<float>::kIncMed;
   static constexpr int kResync = Trig<float>::kResync;
+  IKG_HD static inline void step_med(v2f d, v2f& s, v2f& c) {
+    const v2f d2 = d * d;
+    const v2f sd = d + d * d2 * (-1.0f / 6 + d2 * (1.0f / 120 + d2 * (-1.0f / 5040 + d2 * (1.0f / 362880))));
+    const v2f cd = 1.0f + d2 * (-0.5f + d2 * (1.0f / 24 + d2 * (-1.0f / 720 + d2 * (1.0f / 40320 + d2 * (-1.0f / 3628800)))));
+    const v2f sn = s * cd + c * sd;
+    c = c * cd - s * sd;
+    s = sn;
+  }
   IKG_HD static inline void step(v2f d, v2f& s, v2f& c) {
     const v2f d2 = d * d;
     const v2f sd = d + d * d2 * (-1.0f / 6 + d2 * (1.0f / 120 + d2 * (-1.0f / 5040)));
@@ -1059,7 +1108,13 @@ IKG_HD inline void trig_exact_f1(const KModel<typename LaneT<T>::E>* __restrict_
   add_angles(s[6], c[6], hs, hc, sn[6], cs[6]);
 }
 
-template <typename T>
+// MED: steps beyond the short series' range take a longer series (kIncMed)
+// before falling back to the exact sincos of every slot.  It pays where such
+// steps are common (per-problem seeds: random-seed batches 6.46 -> 5.06 ms fp64,
+// 3.08 -> 2.73 ms fp32 at 131,072) and costs ~5% where they are rare (C2 from
+// q = 0: 0.99 -> 1.04 ms, the extra branch's register pressure), so the
+// launchers pick it per launch (ikg_kernels.hip, ikg_packed.hip).
+template <typename T, bool MED = false>
 IKG_HD inline void trig_advance_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, T qc, const T* qa,
                                    const T* q_old, bool resync, T* sn, T* cs) {
   T dj[7], d[7];
@@ -1073,14 +1128,34 @@ IKG_HD inline void trig_advance_f1(const KModel<typename LaneT<T>::E>* __restric
   d[4] = dj[4];
   d[5] = dj[5];
   d[6] = dj[6];
-  bool big = resync;
+  if constexpr (!MED) {
+    bool big = resync;
 #pragma unroll
-  for (int j = 0; j < 7; ++j) big |= any_of(fabs(d[j]) > T(Trig<T>::kIncMax));
-  // the step always runs in place and the (rare) exact path overwrites it: the
-  // common path then needs no register copies to merge the two
+    for (int j = 0; j < 7; ++j) big |= any_of(fabs(d[j]) > T(Trig<T>::kIncMax));
+    // the step always runs in place and the exact path overwrites it: the
+    // common path then needs no register copies to merge the two
 #pragma unroll
-  for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
-  if (big) trig_exact_f1(m, arm, qc, qa, sn, cs);
+    for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
+    if (big) trig_exact_f1(m, arm, qc, qa, sn, cs);
+    return;
+  }
+  T dmax = fabs(d[0]);
+#pragma unroll
+  for (int j = 1; j < 7; ++j) dmax = fmax(dmax, fabs(d[j]));
+  if (resync || any_of(dmax > T(Trig<T>::kIncMax))) {
+    // steps beyond the short series' range: first steps from random seeds
+    // (multi-start took this path on 14% of its fp64 updates); a longer series
+    // covers them up to kIncMed, the exact sincos beyond and at resyncs
+    if (!resync && all_of(mnot(dmax > T(Trig<T>::kIncMed)))) {
+#pragma unroll
+      for (int j = 0; j < 7; ++j) Trig<T>::step_med(d[j], sn[j], cs[j]);
+    } else {
+      trig_exact_f1(m, arm, qc, qa, sn, cs);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
+  }
 }
 
 // FK + pose error; returns |e|^2 (inverse_geometry.py:58-67; the stop test

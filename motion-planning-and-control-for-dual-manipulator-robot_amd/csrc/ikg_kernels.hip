@@ -37,7 +37,7 @@ namespace ikg {
 #ifndef IKG_WPE
 #define IKG_WPE 0
 #endif
-template <typename T, bool DAMPED, class SP>
+template <typename T, bool DAMPED, class SP, bool MED = false>
 __global__ __launch_bounds__(64)
 #if IKG_WPE
 __attribute__((amdgpu_waves_per_eu(1, IKG_WPE)))
@@ -68,7 +68,7 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
   int it;
   bool conv;
   T nrm, other;
-  solve_pair<T, DAMPED, SP>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
+  solve_pair<T, DAMPED, SP, MED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
   store_q(m, arm, qrow, it, qc, qa, q_out + p * m->nq);
   if (arm == 0) {
     if (conv_out) conv_out[p] = conv ? 1 : 0;
@@ -212,6 +212,16 @@ template <typename T, bool DAMPED, class SP>
 static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
   const int ppw = a.ppw;
   const dim3 grid((unsigned)((a.B + ppw - 1) / ppw));
+  // per-problem seeds (multi-start, or a q0 row per target): large first steps
+  // are common, so the frame-1 loop takes the medium-range trig series
+  if constexpr (kFrame1<SP> && !DAMPED) {
+    if (a.S > 1 || a.q0_stride != 0) {
+      hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, true>), grid, dim3(64), lds_pad_bytes(), s, dmodel,
+                         prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out,
+                         a.converged, a.iters, (T*)a.err_out);
+      return;
+    }
+  }
   hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP>), grid, dim3(64), lds_pad_bytes(), s, dmodel, prm,
                      (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out, a.converged,
                      a.iters, (T*)a.err_out);

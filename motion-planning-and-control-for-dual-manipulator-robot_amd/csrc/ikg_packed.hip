@@ -19,13 +19,15 @@ namespace ikg {
 // v_pk_{fma,mul,add}_f32 advances both arms and a wave holds 64 problems
 // (DESIGN.md §3).  Same loop, same arithmetic as the pair kernel's fp32 path.
 //
-// ONE_WAVE: the kernel claims all 256 AGPRs (an empty asm clobber), so the
-// hardware fits one wave per SIMD.  A launch of at most one wave per SIMD then
-// cannot be dispatched with two waves sharing a SIMD while another idles --
-// which the dispatcher does after some kernels (after the collision
-// continuation, 19-46 of 1,024 SIMDs held two waves of the next 1,024-wave
-// launch and the kernel took 2.2 ms instead of 1.4; tools/placement_probe.py).
-template <class SP, bool ONE_WAVE>
+// WPS (waves per SIMD cap, 0 = none): the kernel claims AGPRs it never uses (an
+// empty asm clobber) so that the hardware fits at most WPS of its waves on a
+// SIMD -- all 256 for WPS = 1; 16 for WPS = 2 (158 VGPRs + 16 > 512 / 3).  A
+// launch of at most WPS waves per SIMD then cannot be dispatched with more
+// waves sharing a SIMD while another idles, which the dispatcher does after
+// some kernels (after the collision continuation, 19-46 of 1,024 SIMDs held two
+// waves of the next 1,024-wave launch and the kernel took 2.2 ms instead of 1.4;
+// tools/placement_probe.py).  The launcher checks the resulting occupancy.
+template <class SP, int WPS, bool MED>
 __global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               KParams<float> prm, const float* __restrict__ targets,
                                                               const float* __restrict__ q0, int64_t q0_stride,
@@ -33,7 +35,8 @@ __global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float
                                                               uint8_t* __restrict__ conv_out,
                                                               int32_t* __restrict__ iters_out,
                                                               float* __restrict__ err_out) {
-  if constexpr (ONE_WAVE) asm volatile("" ::: "a255");
+  if constexpr (WPS == 1) asm volatile("" ::: "a255");
+  if constexpr (WPS == 2) asm volatile("" ::: "a15");
   const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (p >= B) return;
   const int64_t tgt = S > 1 ? p / S : p;
@@ -47,7 +50,7 @@ __global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float
   int it;
   bool conv;
   v2f nrm, other;
-  solve_pair<v2f, false, SP>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
+  solve_pair<v2f, false, SP, MED>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
   float* qo = q_out + p * m->nq;
   qo[m->root_q] = qc.x;
   for (int i = 0; i < m->n_passive; ++i) {  // moved only by the first update's clamp (tools.py:21-22)
@@ -94,18 +97,43 @@ static unsigned simd_count() {
   return v;
 }
 
+// The cap instantiation really fits WPS waves per SIMD (4 WPS single-wave
+// workgroups per CU) on this device; otherwise the uncapped kernel runs.
+template <int WPS>
+static bool capped_ok() {
+  constexpr int kDevs = 64;
+  static std::atomic<int> cache[kDevs];  // 0 unknown, 1 ok, 2 not
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kDevs) return false;
+  int v = cache[dev].load(std::memory_order_relaxed);
+  if (!v) {
+    int blocks = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, false>), 64, packed_lds_pad());
+    v = (e == hipSuccess && blocks == 4 * WPS) ? 1 : 2;
+    cache[dev].store(v, std::memory_order_relaxed);
+  }
+  return v == 1;
+}
+
 hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>& prm, const BatchArgs& a,
                                hipStream_t s) {
   const dim3 grid((unsigned)((a.B + 63) / 64));
-  if (grid.x <= simd_count()) {
-    hipLaunchKernelGGL((ikg_packed_batch_kernel<SpecNextage, true>), grid, dim3(64), packed_lds_pad(), s, dmodel, prm,
-                       (const float*)a.targets, (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out,
-                       a.converged, a.iters, (float*)a.err_out);
-  } else {
-    hipLaunchKernelGGL((ikg_packed_batch_kernel<SpecNextage, false>), grid, dim3(64), packed_lds_pad(), s, dmodel,
-                       prm, (const float*)a.targets, (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out,
-                       a.converged, a.iters, (float*)a.err_out);
-  }
+  const unsigned simds = simd_count();
+  const unsigned need = (grid.x + simds - 1) / simds;  // waves per SIMD the launch needs
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, grid, dim3(64), packed_lds_pad(), s, dmodel, prm, (const float*)a.targets,
+                       (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out, a.converged, a.iters,
+                       (float*)a.err_out);
+  };
+  // per-problem seeds: the medium-range trig series (ikg_device.hpp trig_advance_f1)
+  const bool med = a.S > 1 || a.q0_stride != 0;
+  if (need == 1 && capped_ok<1>())
+    med ? go(ikg_packed_batch_kernel<SpecNextage, 1, true>) : go(ikg_packed_batch_kernel<SpecNextage, 1, false>);
+  else if (need == 2 && capped_ok<2>())
+    med ? go(ikg_packed_batch_kernel<SpecNextage, 2, true>) : go(ikg_packed_batch_kernel<SpecNextage, 2, false>);
+  else
+    med ? go(ikg_packed_batch_kernel<SpecNextage, 0, true>) : go(ikg_packed_batch_kernel<SpecNextage, 0, false>);
   return hipGetLastError();
 }
 

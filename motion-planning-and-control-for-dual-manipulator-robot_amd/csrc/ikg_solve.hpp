@@ -48,7 +48,7 @@ __device__ inline bool both_below(T x, T xo, E eps2) {
 // float: this lane owns one arm (pair layout, partner = lane ^ 1); T = v2f:
 // this lane owns both arms (packed layout).  Returns (through refs) the final
 // q of this lane, the update count and the hand error norms at the returned q.
-template <typename T, bool DAMPED, class SP>
+template <typename T, bool DAMPED, class SP, bool MED = false>
 __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
                                   const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
                                   T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out) {
@@ -125,7 +125,7 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     arm_update(m, arm, T(prm.dt), s, dq, qc, qa, limp);
     ++it;
     if constexpr (F1)
-      trig_advance_f1(m, arm, qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
+      trig_advance_f1<T, MED>(m, arm, qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
     else
       trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }

@@ -22,7 +22,11 @@ dev = torch.device("cuda", 0)
 tdt = torch.float64 if dtype == "f64" else torch.float32
 code = 0 if dtype == "f64" else 1
 tg = torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device=dev)
-q0 = torch.zeros(15, dtype=tdt, device=dev)
+if os.environ.get("ABL_RANDQ0"):  # multi-start-like problems: random seeds (workload.random_seeds)
+    from ikgrasp.workload import random_seeds  # noqa: E402
+    q0 = torch.tensor(random_seeds(load_nextage(), B, seed=1000), dtype=tdt, device=dev)
+else:
+    q0 = torch.zeros(15, dtype=tdt, device=dev)
 qo = torch.empty((B, 15), dtype=tdt, device=dev)
 cv = torch.empty(B, dtype=torch.uint8, device=dev)
 it = torch.empty(B, dtype=torch.int32, device=dev)
@@ -46,7 +50,7 @@ for rnd in range(6):
     for n, lib, h in handles:
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        rc = lib.ikg_solve_batch(h, 0, code, tg.data_ptr(), q0.data_ptr(), 0, B, C.byref(prm), qo.data_ptr(),
+        rc = lib.ikg_solve_batch(h, 0, code, tg.data_ptr(), q0.data_ptr(), 0 if q0.dim() == 1 else 15, B, C.byref(prm), qo.data_ptr(),
                                  cv.data_ptr(), it.data_ptr(), er.data_ptr(), C.c_void_p(s), 0)
         b.record()
         torch.cuda.synchronize()
