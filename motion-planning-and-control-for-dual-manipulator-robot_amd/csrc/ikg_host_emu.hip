@@ -33,7 +33,7 @@ bool emu_collide(const ikg::KModel<T>& m, const ikg::KCollision<T>& c, const T* 
 template <typename T, class SP>
 void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, const T* tg, const T* qrow,
              T* qo, uint8_t* conv_out, int32_t* iters_out, T* err_out, T* trace, int trace_len,
-             const ikg::KCollision<T>* col) {
+             const ikg::KCollision<T>* col, bool med = false) {
   using namespace ikg;
   T RT[2][9], tT[2][3], qc[2], qa[2][kArmDof], sn[2][7], cs[2][7];
   for (int arm = 0; arm < 2; ++arm) {
@@ -125,7 +125,8 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
       load_limits(&m, arm, lim);
       arm_update(&m, arm, prm.dt, s, dq, qc[arm], qa[arm], IKG_LANE_LIMITS ? &lim : nullptr);
       if (f1)
-        trig_advance_f1(&m, arm, qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
+        (med ? trig_advance_f1<T, true> : trig_advance_f1<T, false>)(&m, arm, qc[arm], qa[arm], q_old[arm],
+                                                                     (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
       else
         trig_advance(qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
     }
@@ -163,8 +164,9 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
     const T* qr = (const T*)q0 + stride * i;
     T* tr = trace ? (T*)trace + (int64_t)2 * trace_len * i : nullptr;
     if (spec == 1)
+      // the kernels' medium-range trig series for per-problem seeds (ikg_kernels.hip)
       emu_one<T, ikg::SpecNextage>(m, prm, p->lambda > 0, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
-                                   (T*)err + 2 * i, tr, trace_len, col);
+                                   (T*)err + 2 * i, tr, trace_len, col, stride != 0);
     else if (spec == 2 && !(p->lambda > 0))
       emu_one<T, ikg::SpecGenericWrist>(m, prm, false, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
                                         (T*)err + 2 * i, tr, trace_len, col);
