@@ -122,6 +122,25 @@ void ikg_model_destroy(ikg_model* model);
 /* Attach (or replace) the collision scene of a model. */
 int ikg_model_set_collision(ikg_model* model, const ikg_collision_desc* desc);
 
+/*
+ * Compile the pair-layout kernels against this model's tables (hipRTC, gfx950)
+ * and use them for later ikg_solve_batch / ikg_solve_multistart calls of
+ * `dtype` on `device` that run the pair layout (not PACKED / QUAD).  Joint
+ * axes, identity placements, zero offsets and limits become compile-time
+ * constants; results are those of the prebuilt kernels.  The first call per
+ * model and dtype compiles (about 0.5 s), later devices only load.  `flags`: 0,
+ * or IKG_SPECIALIZE_IF_GENERIC to do nothing (and return IKG_OK) for a model the
+ * prebuilt library already specialises (Nextage class).  Do not call
+ * concurrently with a solve on the same model.  No reference
+ * counterpart: inverse_geometry.py has one Python-level model
+ * (setup_pinocchio.py:73-83); this is the per-model code generation the batched
+ * library adds.
+ */
+#define IKG_SPECIALIZE_IF_GENERIC 1u
+int ikg_model_specialize(ikg_model* model, int device, int dtype, uint32_t flags);
+/* 1 if ikg_model_specialize succeeded for (device, dtype), else 0. */
+int ikg_model_is_specialized(const ikg_model* model, int device, int dtype);
+
 /* Fill `p` with the reference defaults. */
 void ikg_params_default(ikg_params* p);
 

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "ikg_device.hpp"
+#include "ikg_jit.hpp"
 #include "ikg_launch.hpp"
 #include "ikg_model_build.hpp"
 #include "ikgrasp.h"
@@ -50,6 +51,17 @@ struct ikg_model {
   ikg::KCollision<float> c32;
   std::vector<void*> col64;
   std::vector<void*> col32;
+  // model-specialised pair kernels (ikg_model_specialize): code objects per
+  // dtype (0 = f64, 1 = f32), loaded modules per device
+  std::vector<char> jit_code[2];
+  std::vector<ikg::JitKernels*> jit[2];
+
+  template <typename T>
+  const ikg::JitKernels* jit_kernels(int device) {
+    std::lock_guard<std::mutex> lock(mu);
+    const auto& v = jit[sizeof(T) == 8 ? 0 : 1];
+    return device < (int)v.size() ? v[device] : nullptr;
+  }
 
   // Upload `bytes` of `src` to `slot[device]` once; the slot is reused after.
   int upload(std::vector<void*>& slot, int device, const void* src, size_t bytes, const void** out) {
@@ -230,6 +242,7 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
     if (!a.err_out) a.err_out = st.out(sizeof(T) * 2 * B);
     if (st.rc) return st.rc;
   }
+  a.jit = model->jit_kernels<T>(device);
   hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, model->spec, s);
   if (e != hipSuccess) return hip_fail(e, "ikg pair kernel launch");
   if (dc) {
@@ -259,6 +272,7 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   ikg::MultiArgs a{targets, T_, seeds, S, q_out, converged, iters, err_out, best_seed, nq,
                    nullptr, nullptr, nullptr, nullptr};
   a.variant = params->variant;
+  a.jit = model->jit_kernels<T>(device);
   if (params->variant == IKG_VARIANT_PACKED && (sizeof(T) != 4 || model->spec != ikg::kSpecNextage || params->lambda > 0))
     return fail(IKG_EINVAL, "variant PACKED needs fp32, a Nextage-class model and lambda = 0");
   if (params->variant == IKG_VARIANT_QUAD && (model->spec != ikg::kSpecNextage || params->lambda > 0))
@@ -494,6 +508,13 @@ void ikg_model_destroy(ikg_model* m) {
   free_slots(m->dev32);
   free_slots(m->col64);
   free_slots(m->col32);
+  for (auto& v : m->jit)
+    for (size_t i = 0; i < v.size(); ++i)
+      if (v[i]) {
+        (void)hipSetDevice((int)i);
+        ikg::jit_unload(*v[i]);
+        delete v[i];
+      }
   if (prev >= 0) (void)hipSetDevice(prev);
   delete m;
 }
@@ -785,6 +806,81 @@ int ikg_frame_kinematics_batch(const ikg_model* model, int device, int dtype, co
   hipStream_t s = (hipStream_t)stream;
   return dtype == IKG_F64 ? frame_kin_t<double>(m, device, q, v, q_des, v_des, B, rf, *out, s, flags)
                           : frame_kin_t<float>(m, device, q, v, q_des, v_des, B, rf, *out, s, flags);
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ model-specialised kernels
+namespace {
+
+// Compile (once per model and dtype) the pair kernels against this model's
+// tables; the caller holds m->mu.
+int jit_code_locked(ikg_model* m, int dtype) {
+  std::vector<char>& code = m->jit_code[dtype == IKG_F64 ? 0 : 1];
+  if (!code.empty()) return IKG_OK;
+  const std::string src = dtype == IKG_F64 ? ikg::jit_source(m->k64) : ikg::jit_source(m->k32);
+  const std::string err = ikg::jit_compile(src, code);
+  if (!err.empty()) {
+    code.clear();
+    return fail(IKG_EHIP, "model specialisation: %s", err.c_str());
+  }
+  return IKG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ikg_model_specialize(ikg_model* model, int device, int dtype, uint32_t flags) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  if (flags & ~IKG_SPECIALIZE_IF_GENERIC) return fail(IKG_EINVAL, "flags must be 0 or IKG_SPECIALIZE_IF_GENERIC");
+  if ((flags & IKG_SPECIALIZE_IF_GENERIC) && model->spec == ikg::kSpecNextage) return IKG_OK;
+  DeviceGuard g(device);
+  if (g.rc) return g.rc;
+  std::lock_guard<std::mutex> lock(model->mu);
+  auto& slot = model->jit[dtype == IKG_F64 ? 0 : 1];
+  if ((int)slot.size() > device && slot[device]) return IKG_OK;
+  if (int rc = jit_code_locked(model, dtype)) return rc;
+  ikg::JitKernels* k = new (std::nothrow) ikg::JitKernels();
+  if (!k) return fail(IKG_ENOMEM, "out of host memory");
+  const hipError_t e = ikg::jit_load(model->jit_code[dtype == IKG_F64 ? 0 : 1], *k);
+  if (e != hipSuccess) {
+    delete k;
+    return hip_fail(e, "hipModuleLoadData(specialised kernels)");
+  }
+  if ((int)slot.size() <= device) slot.resize(device + 1, nullptr);
+  slot[device] = k;
+  return IKG_OK;
+}
+
+int ikg_model_is_specialized(const ikg_model* model, int device, int dtype) {
+  if (!model || device < 0 || (dtype != IKG_F64 && dtype != IKG_F32)) return 0;
+  ikg_model* m = const_cast<ikg_model*>(model);
+  return dtype == IKG_F64 ? m->jit_kernels<double>(device) != nullptr : m->jit_kernels<float>(device) != nullptr;
+}
+
+// Diagnostic (not in include/ikgrasp.h; no GPU needed): run the specialising
+// compile and report the code object's size; with `path`, also write the code
+// object there (llvm-objdump -d for the ISA).
+int ikg_debug_jit_compile(const ikg_model* model, int dtype, const char* path, size_t* code_size) {
+  g_err[0] = 0;
+  if (!model) return fail(IKG_EINVAL, "model is NULL");
+  if (dtype != IKG_F64 && dtype != IKG_F32) return fail(IKG_EINVAL, "dtype %d unknown", dtype);
+  ikg_model* m = const_cast<ikg_model*>(model);
+  std::lock_guard<std::mutex> lock(m->mu);
+  if (int rc = jit_code_locked(m, dtype)) return rc;
+  const std::vector<char>& code = m->jit_code[dtype == IKG_F64 ? 0 : 1];
+  if (code_size) *code_size = code.size();
+  if (path) {
+    FILE* f = fopen(path, "wb");
+    if (!f) return fail(IKG_EINVAL, "cannot open %s", path);
+    const size_t n = fwrite(code.data(), 1, code.size(), f);
+    fclose(f);
+    if (n != code.size()) return fail(IKG_EINVAL, "short write to %s", path);
+  }
+  return IKG_OK;
 }
 
 }  // extern "C"

@@ -6,7 +6,10 @@
 // the same algorithm and is never linked into this library.
 #pragma once
 
+// (hipRTC, ikg_jit.hip: the runtime compiler provides the HIP declarations)
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
+#endif
 #include <stdint.h>
 
 #include <type_traits>

@@ -26,6 +26,7 @@
 #include "ikg_device.hpp"
 #include "ikgrasp.h"
 #include "ikg_solve.hpp"
+#include "ikg_jit.hpp"
 #include "ikg_launch.hpp"
 
 namespace ikg {
@@ -49,32 +50,11 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             uint8_t* __restrict__ conv_out,
                                                             int32_t* __restrict__ iters_out,
                                                             T* __restrict__ err_out) {
-  const int lane = threadIdx.x;
   // model tables stay in global memory: the compiler hoists them into
   // registers (staging them in LDS and re-reading per iteration measured 8%
   // slower)
-  const KModel<T>* m = gm;
-  const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
-  const int arm = lane & 1;
-  if (lane >= 2 * ppw || p >= B) return;  // both lanes of a pair leave together
-  // multi-start (S > 1): problem p = (target p / S, seed p % S)
-  const int64_t tgt = S > 1 ? p / S : p;
-  const int64_t row = S > 1 ? p - tgt * S : p;
-  T RT[9], tT[3];
-  hook_target(m, arm, targets + tgt * 12, RT, tT);
-  const T* qrow = q0 + row * q0_stride;
-  T qc, qa[kArmDof];
-  load_q(m, arm, qrow, qc, qa);
-  int it;
-  bool conv;
-  T nrm, other;
-  solve_pair<T, DAMPED, SP, MED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
-  store_q(m, arm, qrow, it, qc, qa, q_out + p * m->nq);
-  if (arm == 0) {
-    if (conv_out) conv_out[p] = conv ? 1 : 0;
-    if (iters_out) iters_out[p] = it;
-  }
-  if (err_out) err_out[p * 2 + arm] = nrm;
+  pair_batch_body<T, DAMPED, SP, MED>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
+                                      err_out);
 }
 
 
@@ -291,6 +271,22 @@ hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, con
   }
   if (a.variant == IKG_VARIANT_PACKED) return hipErrorInvalidValue;  // checked by the C-ABI first
   const bool damped = prm.lambda > T(0);
+  if (a.jit) {  // the pair loop compiled against this model's constant tables (ikg_jit.hip)
+    const bool med = a.S > 1 || a.q0_stride != 0;
+    hipFunction_t f = damped ? a.jit->damped : (med && a.jit->pair_med ? a.jit->pair_med : a.jit->pair);
+    const T* targets = (const T*)a.targets;
+    const T* q0 = (const T*)a.q0;
+    T* q_out = (T*)a.q_out;
+    T* err_out = (T*)a.err_out;
+    KParams<T> p = prm;
+    int64_t stride = a.q0_stride, B = a.B, S = a.S;
+    int ppw = a.ppw;
+    uint8_t* conv = a.converged;
+    int32_t* iters = a.iters;
+    void* args[] = {(void*)&dmodel, &p, &targets, &q0, &stride, &B, &S, &ppw, &q_out, &conv, &iters, &err_out};
+    const unsigned grid = (unsigned)((a.B + ppw - 1) / ppw);
+    return hipModuleLaunchKernel(f, grid, 1, 1, 64, 1, 1, (unsigned)lds_pad_bytes(), s, args, nullptr);
+  }
   if (spec == kSpecNextage) {
     if (damped)
       launch_pair_batch_t<T, true, SpecNextage>(dmodel, prm, a, s);
@@ -314,6 +310,7 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   // S == 1: the one seed row serves every target (broadcast), since the batch
   // kernel indexes q0 rows by problem when S == 1
   BatchArgs b{a.targets, a.seeds, a.S == 1 ? 0 : a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
+  b.jit = a.jit;
   // AUTO keeps the pair layout here: seeds spread the update counts, and a
   // wave lasts as long as its slowest problem -- 64 per packed wave against 32
   // per pair wave measured 4.17 ms against 3.66 ms (256 seeds x 512 targets,

@@ -9,6 +9,8 @@
 
 namespace ikg {
 
+struct JitKernels;  // ikg_jit.hpp
+
 struct BatchArgs {
   const void* targets;
   const void* q0;
@@ -21,6 +23,8 @@ struct BatchArgs {
   int ppw;         // problems per 64-lane wave (1..32)
   int64_t S = 1;   // seeds per target (multi-start): problem p = (target p / S, q0 row p % S)
   int variant = 0; // ikg_variant
+  // model-specialised pair kernels on this device (ikg_model_specialize), or null
+  const JitKernels* jit = nullptr;
 };
 
 struct MultiArgs {
@@ -44,6 +48,7 @@ struct MultiArgs {
   const void* collision = nullptr;
   int n_geoms = 0;
   int variant = 0;  // ikg_variant of the per-seed solves
+  const JitKernels* jit = nullptr;
 };
 
 // kernel specialisation chosen at model creation (ikg_model_build.hpp)

@@ -141,4 +141,38 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   conv_out = conv;
 }
 
+// Pair-layout batch kernel body (ikg_kernels.hip ikg_pair_batch_kernel, and the
+// model-specialised kernels ikg_jit.cpp compiles at run time with `m` pointing
+// at a constant copy of the model tables): one 64-lane wave per workgroup
+// holding `ppw` problems on lanes [0, 2 ppw).
+template <typename T, bool DAMPED, class SP, bool MED>
+__device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KParams<T>& prm,
+                                       const T* __restrict__ targets, const T* __restrict__ q0, int64_t q0_stride,
+                                       int64_t B, int64_t S, int ppw, T* __restrict__ q_out,
+                                       uint8_t* __restrict__ conv_out, int32_t* __restrict__ iters_out,
+                                       T* __restrict__ err_out) {
+  const int lane = threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
+  const int arm = lane & 1;
+  if (lane >= 2 * ppw || p >= B) return;  // both lanes of a pair leave together
+  // multi-start (S > 1): problem p = (target p / S, seed p % S)
+  const int64_t tgt = S > 1 ? p / S : p;
+  const int64_t row = S > 1 ? p - tgt * S : p;
+  T RT[9], tT[3];
+  hook_target(m, arm, targets + tgt * 12, RT, tT);
+  const T* qrow = q0 + row * q0_stride;
+  T qc, qa[kArmDof];
+  load_q(m, arm, qrow, qc, qa);
+  int it;
+  bool conv;
+  T nrm, other;
+  solve_pair<T, DAMPED, SP, MED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
+  store_q(m, arm, qrow, it, qc, qa, q_out + p * m->nq);
+  if (arm == 0) {
+    if (conv_out) conv_out[p] = conv ? 1 : 0;
+    if (iters_out) iters_out[p] = it;
+  }
+  if (err_out) err_out[p * 2 + arm] = nrm;
+}
+
 }  // namespace ikg

@@ -17,6 +17,7 @@ IKG_ARM_DOF = 6
 IKG_F64, IKG_F32 = 0, 1
 IKG_FLAG_HOST_POINTERS = 1
 IKG_VARIANT_AUTO, IKG_VARIANT_PAIR, IKG_VARIANT_PACKED, IKG_VARIANT_QUAD = 0, 1, 2, 3
+IKG_SPECIALIZE_IF_GENERIC = 1
 # pinocchio.ReferenceFrame values (ikg_reference_frame)
 IKG_WORLD, IKG_LOCAL, IKG_LOCAL_WORLD_ALIGNED = 0, 1, 2
 
@@ -83,7 +84,7 @@ EXPORTS = [
     "ikg_model_create", "ikg_model_destroy", "ikg_params_default", "ikg_solve_batch",
     "ikg_solve_multistart", "ikg_fk_batch", "ikg_log6_batch", "ikg_last_error", "ikg_version",
     "ikg_model_set_collision", "ikg_collision_batch", "ikg_distance_batch", "ikg_target_env_batch",
-    "ikg_frame_kinematics_batch",
+    "ikg_frame_kinematics_batch", "ikg_model_specialize", "ikg_model_is_specialized",
 ]
 
 _lib = None
@@ -145,6 +146,12 @@ def load() -> C.CDLL:
     lib.ikg_frame_kinematics_batch.argtypes = [vp, i32, i32, vp, vp, vp, vp, i64, i32, C.POINTER(FrameKinOut), vp,
                                                C.c_uint32]
     lib.ikg_frame_kinematics_batch.restype = i32
+    lib.ikg_model_specialize.argtypes = [vp, i32, i32, C.c_uint32]
+    lib.ikg_model_specialize.restype = i32
+    lib.ikg_model_is_specialized.argtypes = [vp, i32, i32]
+    lib.ikg_model_is_specialized.restype = i32
+    lib.ikg_debug_jit_compile.argtypes = [vp, i32, C.c_char_p, C.POINTER(C.c_size_t)]
+    lib.ikg_debug_jit_compile.restype = i32
     lib.ikg_last_error.argtypes = []
     lib.ikg_last_error.restype = C.c_char_p
     lib.ikg_version.argtypes = []

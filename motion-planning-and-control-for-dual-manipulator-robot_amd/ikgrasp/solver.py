@@ -8,6 +8,7 @@ benchmark uses).  The HIP kernel is the only compute path.
 from __future__ import annotations
 
 import ctypes as C
+import warnings
 from dataclasses import dataclass
 
 import numpy as np
@@ -62,8 +63,17 @@ class Solution:
 class IKSolver:
     """Owns one native model (`ikg_model_create`)."""
 
-    def __init__(self, model: DualArmModel | None = None, device: int = 0, scene=None):
-        """`scene`: an ikgrasp.collision.CollisionScene to attach (see set_collision)."""
+    def __init__(self, model: DualArmModel | None = None, device: int = 0, scene=None, specialize="auto"):
+        """`scene`: an ikgrasp.collision.CollisionScene to attach (see set_collision).
+        `specialize`: "auto" compiles model-specialised pair kernels
+        (ikg_model_specialize) on a model's first solve per dtype and device
+        unless the prebuilt library already has its specialisation (Nextage
+        class); a failed compile warns and keeps the prebuilt generic kernel.
+        True: always specialise, raising on failure.  False: prebuilt only."""
+        if specialize not in ("auto", True, False):
+            raise ValueError(f"specialize must be 'auto', True or False, got {specialize!r}")
+        self._specialize = specialize
+        self._specialized = set()
         self.lib = _lib.load()
         self.model = model if model is not None else load_nextage()
         self.desc = _lib.model_desc(self.model)
@@ -81,6 +91,37 @@ class IKSolver:
         self._cdesc = _lib.collision_desc(scene)
         _lib.check(self.lib.ikg_model_set_collision(self._h, C.byref(self._cdesc)))
         self.scene = scene
+
+    def _auto_specialize(self, device, code):
+        if self._specialize is False or (device, code) in self._specialized:
+            return
+        self._specialized.add((device, code))
+        flags = _lib.IKG_SPECIALIZE_IF_GENERIC if self._specialize == "auto" else 0
+        rc = self.lib.ikg_model_specialize(self._h, device, code, flags)
+        if rc != 0:
+            msg = self.lib.ikg_last_error().decode()
+            if self._specialize is True:
+                raise _lib.IkgError(rc, msg)
+            warnings.warn(f"model specialisation failed, using the prebuilt generic kernels: {msg}")
+
+    def _native_solve(self, h, device, code, *rest):
+        self._auto_specialize(device, code)
+        return self.lib.ikg_solve_batch(h, device, code, *rest)
+
+    def _native_multistart(self, h, device, code, *rest):
+        self._auto_specialize(device, code)
+        return self.lib.ikg_solve_multistart(h, device, code, *rest)
+
+    def specialize(self, dtype="f64", device=None):
+        """Compile the pair-layout kernels against this model's tables
+        (ikg_model_specialize, hipRTC) for `dtype` on `device` (default: the
+        solver's); later solves there use them.  Seconds for the first device."""
+        code, _ = _dtype(dtype)
+        _lib.check(self.lib.ikg_model_specialize(self._h, self.device if device is None else device, code, 0))
+
+    def is_specialized(self, dtype="f64", device=None) -> bool:
+        code, _ = _dtype(dtype)
+        return bool(self.lib.ikg_model_is_specialized(self._h, self.device if device is None else device, code))
 
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
@@ -119,7 +160,7 @@ class IKSolver:
         conv = np.empty(B, dtype=np.uint8)
         iters = np.empty(B, dtype=np.int32)
         err = np.empty((B, 2), dtype=npt)
-        _lib.check(self.lib.ikg_solve_batch(
+        _lib.check(self._native_solve(
             self._h, self.device, code, tg.ctypes.data, q.ctypes.data, stride, B, C.byref(prm),
             q_out.ctypes.data, conv.ctypes.data, iters.ctypes.data, err.ctypes.data, None,
             _lib.IKG_FLAG_HOST_POINTERS))
@@ -140,7 +181,7 @@ class IKSolver:
         iters = torch.empty(B, dtype=torch.int32, device=dev)
         err = torch.empty((B, 2), dtype=targets.dtype, device=dev)
         s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
-        _lib.check(self.lib.ikg_solve_batch(
+        _lib.check(self._native_solve(
             self._h, dev.index or 0, code, tg.data_ptr(), q.data_ptr(), stride, B, C.byref(prm),
             q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(), err.data_ptr(), C.c_void_p(s), 0))
         return Solution(q_out, conv.bool(), iters, err)
@@ -149,7 +190,7 @@ class IKSolver:
         """Raw device-pointer launch (all tensors preallocated; used by bench.py)."""
         prm = self.params(**kw)
         stride = _q0_stride(q0.shape, targets.shape[0], self.nq)
-        _lib.check(self.lib.ikg_solve_batch(
+        _lib.check(self._native_solve(
             self._h, targets.device.index or 0, dtype_code, targets.data_ptr(), q0.data_ptr(), stride,
             targets.shape[0], C.byref(prm), q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(),
             err.data_ptr(), C.c_void_p(stream_handle), 0))
@@ -159,7 +200,7 @@ class IKSolver:
         prm = self.params(**kw)
         if seeds.dim() != 2 or seeds.shape[1] != self.nq:
             raise ValueError(f"seeds must be [S,{self.nq}], got {list(seeds.shape)}")
-        _lib.check(self.lib.ikg_solve_multistart(
+        _lib.check(self._native_multistart(
             self._h, targets.device.index or 0, dtype_code, targets.data_ptr(), targets.shape[0], seeds.data_ptr(),
             seeds.shape[0], C.byref(prm), q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(), err.data_ptr(),
             best.data_ptr(), C.c_void_p(stream_handle), 0))
@@ -177,7 +218,7 @@ class IKSolver:
         iters = np.empty(T, dtype=np.int32)
         err = np.empty((T, 2), dtype=npt)
         best = np.empty(T, dtype=np.int32)
-        _lib.check(self.lib.ikg_solve_multistart(
+        _lib.check(self._native_multistart(
             self._h, self.device, code, tg.ctypes.data, T, sd.ctypes.data, S, C.byref(prm),
             q_out.ctypes.data, conv.ctypes.data, iters.ctypes.data, err.ctypes.data, best.ctypes.data, None,
             _lib.IKG_FLAG_HOST_POINTERS))

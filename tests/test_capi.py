@@ -113,3 +113,23 @@ def test_no_device_fails_loudly_without_gpu():
     s = IKSolver()
     with pytest.raises(_lib.IkgError):
         s.solve(np.zeros((1, 12)), np.zeros(15))
+
+
+@pytest.mark.parametrize("which", ["nextage", "tilted"])
+def test_specialising_compile_runs_on_cpu(which):
+    """ikg_model_specialize's hipRTC step (no GPU needed): the library's embedded
+    device headers compile against a model's constant tables, both dtypes."""
+    from ikgrasp.model import DualArmModel
+    from ikgrasp.solver import IKSolver
+    from conftest import GOLDEN
+    m = load_nextage() if which == "nextage" else DualArmModel.from_urdf(
+        os.path.join(GOLDEN, "tilted_dualarm.urdf"), os.path.join(GOLDEN, "tilted_cube.urdf"))
+    s = IKSolver(m)
+    n = C.c_size_t()
+    for dtype in (_lib.IKG_F64, _lib.IKG_F32):
+        rc = s.lib.ikg_debug_jit_compile(s._h, dtype, None, C.byref(n))
+        assert rc == 0, s.lib.ikg_last_error().decode()
+        assert n.value > 4096
+    assert s.lib.ikg_model_specialize(s._h, 0, _lib.IKG_F64, 6) == -1
+    assert "flags" in s.lib.ikg_last_error().decode()
+    s.close()

@@ -1,7 +1,9 @@
 """Generic-path benchmark: the synthetic tilted-axis robot
 (tests/golden/tilted_dualarm.urdf: runtime axes, placement rotations,
 Householder-QR arm solve) against the Nextage specialisation, same batch and
-dtype, device-resident inputs, HIP events on the launch stream.  One JSON line.
+dtype, device-resident inputs, HIP events on the launch stream; each model also
+through its run-time specialised kernels (ikg_model_specialize, with the
+compile + load time).  One JSON line.
     python tools/generic_bench.py [--batch 4096] [--dtype f64]"""
 import argparse
 import ctypes as C
@@ -57,13 +59,22 @@ def main():
     tg = np.repeat(g["targets"][:1], B, axis=0)
     tg[:, 9:] += rng.uniform(-0.05, 0.05, (B, 3))
     tilted = IKSolver(DualArmModel.from_urdf(os.path.join(GOLDEN, "tilted_dualarm.urdf"),
-                                             os.path.join(GOLDEN, "tilted_cube.urdf")))
-    nextage = IKSolver()
+                                             os.path.join(GOLDEN, "tilted_cube.urdf")), specialize=False)
+    nextage = IKSolver(specialize=False)
     out = {"bench": "generic path (SURVEY 8f-3)", "batch": B, "dtype": a.dtype}
     out["tilted_generic"] = time_solver(tilted, torch.tensor(tg, dtype=tdt, device="cuda"),
                                         torch.zeros(tilted.nq, dtype=tdt, device="cuda"), a.steps, code)
     out["nextage_specialised"] = time_solver(nextage, torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device="cuda"),
                                              torch.zeros(nextage.nq, dtype=tdt, device="cuda"), a.steps, code)
+    import time
+    for name, sv in (("tilted", tilted), ("nextage", nextage)):
+        t0 = time.time()
+        sv.specialize(a.dtype)
+        out[f"{name}_specialize_s"] = time.time() - t0
+    out["tilted_jit"] = time_solver(tilted, torch.tensor(tg, dtype=tdt, device="cuda"),
+                                    torch.zeros(tilted.nq, dtype=tdt, device="cuda"), a.steps, code)
+    out["nextage_jit"] = time_solver(nextage, torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device="cuda"),
+                                     torch.zeros(nextage.nq, dtype=tdt, device="cuda"), a.steps, code)
     print(json.dumps(out))
 
 
