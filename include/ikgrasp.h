@@ -55,9 +55,9 @@ enum ikg_status {
 
 /* kernel variant selector (ikg_params.variant) */
 enum ikg_variant {
-  IKG_VARIANT_AUTO = 0,   /* ikg_solve_batch: QUAD where it applies and B <= 8,192 (the batch
-                             leaves SIMDs idle), PACKED where it applies and B > 4 pair waves
-                             per CU, else PAIR; ikg_solve_multistart: PAIR */
+  IKG_VARIANT_AUTO = 0,   /* ikg_solve_batch: PACKED where it applies and B > 4 pair waves
+                             per CU, else PAIR (QUAD measured no faster: explicit only);
+                             ikg_solve_multistart: PAIR */
   IKG_VARIANT_PAIR = 1,   /* two lanes per problem (one arm per lane), 32 problems / wave */
   IKG_VARIANT_PACKED = 2, /* fp32, Nextage-class models, lambda = 0: one lane per problem with
                              both arms packed in 2-vectors (v_pk_*_f32), 64 problems / wave */
