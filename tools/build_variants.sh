@@ -8,7 +8,7 @@ rm -f ../ikgrasp/_native/var/*.so
 while [ $# -gt 0 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-slp-vectorize -Xarch_device -ffinite-math-only -Xarch_device -fno-signed-zeros -Xarch_device -Wno-nan-infinity-disabled $flags -I../../include -I. \
-    -shared -o ../ikgrasp/_native/var/lib_$name.so ikg_kernels.hip ikg_packed.hip ikg_quad.hip ikg_collision.hip ikg_control.hip ikg_capi.hip &
+    -shared -o ../ikgrasp/_native/var/lib_$name.so ikg_kernels.hip ikg_packed.hip ikg_quad.hip ikg_collision.hip ikg_control.hip ikg_jit.hip ikg_capi.hip -ldl &
 done
 wait
 ls ../ikgrasp/_native/var
