@@ -22,6 +22,11 @@ SETS = {
     "all": ("placement", "velocity", "J", "dJ", "dJv", "err", "derr"),
     "task": ("placement", "velocity", "J", "dJv", "err", "derr"),  # control.task_space_terms
     "jac": ("J", "dJ"),
+    # breakdown of the task set
+    "J": ("J",),
+    "pv": ("placement", "velocity"),
+    "pvj": ("placement", "velocity", "J", "dJv"),
+    "err": ("err", "derr"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md
 
