@@ -186,9 +186,31 @@ class IKSolver:
             q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(), err.data_ptr(), C.c_void_p(s), 0))
         return Solution(q_out, conv.bool(), iters, err)
 
+    def _check_out(self, B, dtype_code, targets, q_out, conv, iters, err, best=None):
+        """Preallocated torch buffers of the raw launches: shapes, dtypes and
+        contiguity the kernels assume (a q_out narrower than nq would be
+        written past its end)."""
+        import torch
+        fdt = torch.float64 if dtype_code == _lib.IKG_F64 else torch.float32
+        want = [(targets, (B, 12), fdt, "targets"), (q_out, (B, self.nq), fdt, "q_out"),
+                (conv, (B,), torch.uint8, "converged"), (iters, (B,), torch.int32, "iters"),
+                (err, (B, 2), fdt, "err")]
+        if best is not None:
+            want.append((best, (B,), torch.int32, "best_seed"))
+        for t, shape, dt, name in want:
+            if tuple(t.shape) != shape or t.dtype != dt or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous {dt} tensor of shape {list(shape)}, got "
+                                 f"{t.dtype} {list(t.shape)}")
+        for t, _, _, name in want:
+            if not t.is_cuda:
+                raise ValueError(f"{name} must be a device tensor")
+
     def solve_into(self, targets, q0, q_out, conv, iters, err, dtype_code, stream_handle, **kw):
         """Raw device-pointer launch (all tensors preallocated; used by bench.py)."""
         prm = self.params(**kw)
+        self._check_out(targets.shape[0], dtype_code, targets, q_out, conv, iters, err)
+        if not q0.is_contiguous() or q0.dtype != targets.dtype:
+            raise ValueError("q0 must be contiguous and of the targets' dtype")
         stride = _q0_stride(q0.shape, targets.shape[0], self.nq)
         _lib.check(self._native_solve(
             self._h, targets.device.index or 0, dtype_code, targets.data_ptr(), q0.data_ptr(), stride,
@@ -200,6 +222,9 @@ class IKSolver:
         prm = self.params(**kw)
         if seeds.dim() != 2 or seeds.shape[1] != self.nq:
             raise ValueError(f"seeds must be [S,{self.nq}], got {list(seeds.shape)}")
+        if not seeds.is_contiguous() or seeds.dtype != targets.dtype:
+            raise ValueError("seeds must be contiguous and of the targets' dtype")
+        self._check_out(targets.shape[0], dtype_code, targets, q_out, conv, iters, err, best)
         _lib.check(self._native_multistart(
             self._h, targets.device.index or 0, dtype_code, targets.data_ptr(), targets.shape[0], seeds.data_ptr(),
             seeds.shape[0], C.byref(prm), q_out.data_ptr(), conv.data_ptr(), iters.data_ptr(), err.data_ptr(),

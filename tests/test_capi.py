@@ -133,3 +133,26 @@ def test_specialising_compile_runs_on_cpu(which):
     assert s.lib.ikg_model_specialize(s._h, 0, _lib.IKG_F64, 6) == -1
     assert "flags" in s.lib.ikg_last_error().decode()
     s.close()
+
+
+def test_raw_launch_buffer_checks():
+    """solve_into / solve_multistart_into reject buffers the kernels would
+    overrun or misread, before any device call (CPU tensors fail the device check)."""
+    import torch
+    from ikgrasp.solver import IKSolver
+    s = IKSolver()
+    B = 4
+    tg = torch.zeros((B, 12), dtype=torch.float64)
+    good = dict(q_out=torch.zeros((B, 15), dtype=torch.float64), conv=torch.zeros(B, dtype=torch.uint8),
+                iters=torch.zeros(B, dtype=torch.int32), err=torch.zeros((B, 2), dtype=torch.float64))
+    with pytest.raises(ValueError, match="device tensor"):  # CPU tensors, shapes right
+        s.solve_into(tg, torch.zeros(15, dtype=torch.float64), *good.values(), _lib.IKG_F64, 0)
+    bad = dict(good, q_out=torch.zeros((B, 14), dtype=torch.float64))
+    with pytest.raises(ValueError, match="q_out"):
+        s._check_out(B, _lib.IKG_F64, tg, *bad.values())
+    bad = dict(good, iters=torch.zeros(B, dtype=torch.int64))
+    with pytest.raises(ValueError, match="iters"):
+        s._check_out(B, _lib.IKG_F64, tg, *bad.values())
+    with pytest.raises(ValueError, match="q_out"):  # fp32 launch code, fp64 buffers
+        s._check_out(B, _lib.IKG_F32, tg.float(), *good.values())
+    s.close()
