@@ -127,11 +127,14 @@ int ikg_model_set_collision(ikg_model* model, const ikg_collision_desc* desc);
  * and use them for later ikg_solve_batch / ikg_solve_multistart calls of
  * `dtype` on `device` that run the pair layout (not PACKED / QUAD).  Joint
  * axes, identity placements, zero offsets and limits become compile-time
- * constants; results are those of the prebuilt kernels.  The first call per
+ * constants; results match the prebuilt kernels' (same flags and update
+ * counts, q to rounding: folded exact 0 / 1 terms).  The first call per
  * model and dtype compiles (about 0.5 s), later devices only load.  `flags`: 0,
  * or IKG_SPECIALIZE_IF_GENERIC to do nothing (and return IKG_OK) for a model the
  * prebuilt library already specialises (Nextage class).  Do not call
- * concurrently with a solve on the same model.  No reference
+ * concurrently with a solve on the same model.  With the environment variable
+ * IKG_JIT_CACHE_DIR set, code objects are cached there (keyed by the generated
+ * source, the embedded device headers and the compile options).  No reference
  * counterpart: inverse_geometry.py has one Python-level model
  * (setup_pinocchio.py:73-83); this is the per-model code generation the batched
  * library adds.

@@ -156,3 +156,23 @@ def test_raw_launch_buffer_checks():
     with pytest.raises(ValueError, match="q_out"):  # fp32 launch code, fp64 buffers
         s._check_out(B, _lib.IKG_F32, tg.float(), *good.values())
     s.close()
+
+
+def test_specialising_compile_cache(tmp_path, monkeypatch):
+    """IKG_JIT_CACHE_DIR: the first compile writes the code object, a second
+    model with the same tables loads it without compiling (and gets the same bytes)."""
+    import time
+    from ikgrasp.solver import IKSolver
+    monkeypatch.setenv("IKG_JIT_CACHE_DIR", str(tmp_path))
+    n = C.c_size_t()
+    a = IKSolver()
+    assert a.lib.ikg_debug_jit_compile(a._h, _lib.IKG_F32, str(tmp_path / "a.co").encode(), C.byref(n)) == 0
+    files = sorted(p.name for p in tmp_path.glob("ikg_jit_*.co"))
+    assert len(files) == 1
+    b = IKSolver()
+    t0 = time.perf_counter()
+    assert b.lib.ikg_debug_jit_compile(b._h, _lib.IKG_F32, str(tmp_path / "b.co").encode(), C.byref(n)) == 0
+    assert time.perf_counter() - t0 < 0.5  # a hipRTC compile takes ~1.5 s here
+    assert (tmp_path / "a.co").read_bytes() == (tmp_path / "b.co").read_bytes()
+    a.close()
+    b.close()
