@@ -100,10 +100,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # IKG_BENCH_BACKEND=gloo: rehearsal of the multi-rank path on a box with
+    # fewer GPUs than ranks (ranks share devices, collectives on host copies);
+    # the measured configuration is RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("IKG_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    host = backend != "nccl"  # collectives on host copies
 
     from ikgrasp import _lib
     from ikgrasp.solver import IKSolver
@@ -124,7 +134,8 @@ def main():
     conv = torch.empty(B, dtype=torch.uint8, device=dev)
     iters = torch.empty(B, dtype=torch.int32, device=dev)
     err = torch.empty((B, 2), dtype=tdt, device=dev)
-    gathered = [torch.empty_like(q_out) for _ in range(world)] if (world > 1 and rank == 0) else None
+    gathered = ([torch.empty_like(q_out, device="cpu" if host else dev) for _ in range(world)]
+                if (world > 1 and rank == 0) else None)
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
     S = args.multistart
@@ -146,7 +157,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if world > 1 and not args.no_gather:
-            dist.gather(q_out, gathered, dst=0)
+            dist.gather(q_out.cpu() if host else q_out, gathered, dst=0)
 
     for _ in range(args.warmup):
         step()
@@ -183,7 +194,8 @@ def main():
         torch.cuda.synchronize()
         sum_iters = int(i_x.to(torch.int64).sum().item())
         del tg_x, q0_x, q_x, c_x, i_x, e_x
-    stats = torch.tensor([elapsed, kern_ms, n_conv, B, sum_iters], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, kern_ms, n_conv, B, sum_iters], dtype=torch.float64,
+                         device="cpu" if host else dev)
     if world > 1:
         t_max = stats[:2].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -237,7 +249,8 @@ def main():
                 "collision_term": bool(args.collision),
                 "seeds_per_target": S or 1,
                 "batch_per_gpu": B, "global_batch": B * world, "yaw_range": args.yaw,
-                "parallelism": f"shard{world}" + ("" if world == 1 or args.no_gather else "+rccl_gather_q"),
+                "parallelism": f"shard{world}" + ("" if world == 1 or args.no_gather else
+                                                  ("+rccl_gather_q" if not host else "+gloo_gather_q")),
             },
             "problems_per_s": tot_B / per_step,
             "converged_fraction": tot_conv / tot_B,
