@@ -55,58 +55,12 @@ __device__ inline void cross3(const T* a, const T* b, T* c) {
   c[2] = a[0] * b[1] - a[1] * b[0];
 }
 
-// sin/cos of a joint angle: Cody-Waite reduction by pi/2 in three FMA parts
-// and Taylor polynomials on |r| <= pi/4 (truncation < 1e-17; ~1 ulp overall).
-// The reduction stays within ~1e-16 absolute for |x| < 2^40 (fp64; fp32:
-// |x| < 2^16), far beyond any joint angle.  It replaces OCML's sincos, whose
+// sin/cos of a joint angle: ikg_device.hpp cw_sincos (Cody-Waite reduction and
+// Taylor polynomials).  It replaced OCML's sincos here first, whose
 // Payne-Hanek path for huge arguments dominated the code of the first version.
 template <typename T>
 __device__ inline void joint_sincos(T x, T* s, T* c) {
-  const T n = rint(x * T(0.63661977236758134308));  // 2/pi
-  T r;
-  if constexpr (sizeof(T) == 8) {
-    r = fma(-n, 1.5707963267948966, x);
-    r = fma(-n, 6.123233995736766e-17, r);
-    r = fma(-n, -1.4973849048591698e-33, r);
-  } else {
-    r = fmaf(-n, 1.57079637f, x);
-    r = fmaf(-n, -4.37113883e-08f, r);
-    r = fmaf(-n, -1.71512489e-15f, r);
-  }
-  const T r2 = r * r;
-  T sp, cp;
-  if constexpr (sizeof(T) == 8) {  // sin: r (1 - r^2/3! + ... - r^14/15!), cos: 1 - r^2/2! + ... + r^16/16!
-    sp = T(-1.0 / 1307674368000.0);
-    sp = fma(sp, r2, T(1.0 / 6227020800.0));
-    sp = fma(sp, r2, T(-1.0 / 39916800.0));
-    sp = fma(sp, r2, T(1.0 / 362880.0));
-    sp = fma(sp, r2, T(-1.0 / 5040.0));
-    sp = fma(sp, r2, T(1.0 / 120.0));
-    sp = fma(sp, r2, T(-1.0 / 6.0));
-    cp = T(1.0 / 20922789888000.0);
-    cp = fma(cp, r2, T(-1.0 / 87178291200.0));
-    cp = fma(cp, r2, T(1.0 / 479001600.0));
-    cp = fma(cp, r2, T(-1.0 / 3628800.0));
-    cp = fma(cp, r2, T(1.0 / 40320.0));
-    cp = fma(cp, r2, T(-1.0 / 720.0));
-    cp = fma(cp, r2, T(1.0 / 24.0));
-  } else {
-    sp = T(1.0 / 362880.0);
-    sp = fmaf(sp, r2, T(-1.0 / 5040.0));
-    sp = fmaf(sp, r2, T(1.0 / 120.0));
-    sp = fmaf(sp, r2, T(-1.0 / 6.0));
-    cp = T(-1.0 / 3628800.0);
-    cp = fmaf(cp, r2, T(1.0 / 40320.0));
-    cp = fmaf(cp, r2, T(-1.0 / 720.0));
-    cp = fmaf(cp, r2, T(1.0 / 24.0));
-  }
-  const T sr = fma(r * r2, sp, r);
-  const T cr = fma(r2 * r2, cp, fma(r2, T(-0.5), T(1)));
-  const int qd = (int)n & 3;
-  const T ss = (qd & 1) ? cr : sr;
-  const T cc = (qd & 1) ? sr : cr;
-  *s = (qd & 2) ? -ss : ss;
-  *c = ((qd + 1) & 2) ? -cc : cc;
+  cw_sincos(x, s, c);
 }
 
 // R <- R Rot_axis(s, c) and a = the axis column of R (unchanged by the

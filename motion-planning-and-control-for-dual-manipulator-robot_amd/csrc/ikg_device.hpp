@@ -207,6 +207,80 @@ IKG_HD inline v2f atan2(v2f y, v2f x) { return v2f{::atan2f(y.x, x.x), ::atan2f(
 IKG_HD inline v2f atan2f(v2f y, v2f x) { return atan2(y, x); }
 
 // ---------------------------------------------------------------- precision traits
+// sin/cos of a joint angle: Cody-Waite reduction by pi/2 in three FMA parts
+// and Taylor polynomials on |r| <= pi/4 (truncation < 5e-17 fp64, < 2e-9
+// fp32; ~1 ulp overall).  The reduction stays within ~1e-16 absolute for
+// |x| < 2^40 (fp64; fp32: |x| < 2^16), far beyond any joint angle.  It replaces
+// OCML's sincos, whose Payne-Hanek path for huge arguments is dead weight in
+// the loop's exact trig (every 16th fp32 update: IKG_CW_SINCOS=0 restores it).
+#ifndef IKG_CW_SINCOS
+#define IKG_CW_SINCOS 1
+#endif
+template <typename T>
+IKG_HD inline void cw_poly(T r, T& sr, T& cr) {
+  const T r2 = r * r;
+  T sp, cp;
+  if constexpr (std::is_same<T, double>::value) {  // sin: r (1 - r^2/3! + ... - r^14/15!), cos: to r^16/16!
+    sp = T(-1.0 / 1307674368000.0);
+    sp = fma(sp, r2, T(1.0 / 6227020800.0));
+    sp = fma(sp, r2, T(-1.0 / 39916800.0));
+    sp = fma(sp, r2, T(1.0 / 362880.0));
+    sp = fma(sp, r2, T(-1.0 / 5040.0));
+    sp = fma(sp, r2, T(1.0 / 120.0));
+    sp = fma(sp, r2, T(-1.0 / 6.0));
+    cp = T(1.0 / 20922789888000.0);
+    cp = fma(cp, r2, T(-1.0 / 87178291200.0));
+    cp = fma(cp, r2, T(1.0 / 479001600.0));
+    cp = fma(cp, r2, T(-1.0 / 3628800.0));
+    cp = fma(cp, r2, T(1.0 / 40320.0));
+    cp = fma(cp, r2, T(-1.0 / 720.0));
+    cp = fma(cp, r2, T(1.0 / 24.0));
+    sr = fma(r * r2, sp, r);
+    cr = fma(r2 * r2, cp, fma(r2, T(-0.5), T(1)));
+  } else {  // float or the packed pair (contracted to v_pk_fma_f32)
+    sp = T(1.0f / 362880.0f);
+    sp = sp * r2 + T(-1.0f / 5040.0f);
+    sp = sp * r2 + T(1.0f / 120.0f);
+    sp = sp * r2 + T(-1.0f / 6.0f);
+    cp = T(-1.0f / 3628800.0f);
+    cp = cp * r2 + T(1.0f / 40320.0f);
+    cp = cp * r2 + T(-1.0f / 720.0f);
+    cp = cp * r2 + T(1.0f / 24.0f);
+    sr = (r * r2) * sp + r;
+    cr = (r2 * r2) * cp + (r2 * T(-0.5f) + T(1.0f));
+  }
+}
+
+// quadrant n (mod 4) of the reduction: (sin, cos)(r + n pi/2)
+template <typename T>
+IKG_HD inline void cw_quadrant(int n, T sr, T cr, T* s, T* c) {
+  const int qd = n & 3;
+  const T ss = (qd & 1) ? cr : sr;
+  const T cc = (qd & 1) ? sr : cr;
+  *s = (qd & 2) ? -ss : ss;
+  *c = ((qd + 1) & 2) ? -cc : cc;
+}
+
+IKG_HD inline void cw_sincos(double x, double* s, double* c) {
+  const double n = rint(x * 0.63661977236758134308);  // 2/pi
+  double r = fma(-n, 1.5707963267948966, x);
+  r = fma(-n, 6.123233995736766e-17, r);
+  r = fma(-n, -1.4973849048591698e-33, r);
+  double sr, cr;
+  cw_poly(r, sr, cr);
+  cw_quadrant((int)n, sr, cr, s, c);
+}
+
+IKG_HD inline void cw_sincos(float x, float* s, float* c) {
+  const float n = rintf(x * 0.636619772f);
+  float r = fmaf(-n, 1.57079637f, x);
+  r = fmaf(-n, -4.37113883e-08f, r);
+  r = fmaf(-n, -1.71512489e-15f, r);
+  float sr, cr;
+  cw_poly(r, sr, cr);
+  cw_quadrant((int)n, sr, cr, s, c);
+}
+
 template <typename T>
 struct Prec;
 
@@ -217,7 +291,13 @@ struct Prec<double> {
   static constexpr double kPi = 3.14159265358979323846;
   // relative cut-off for the triangular solve (np.linalg.pinv rcond = 1e-15)
   static constexpr double kRcond = 1e-15;
-  IKG_HD static inline void sincos_(double x, double* s, double* c) { ::sincos(x, s, c); }
+  IKG_HD static inline void sincos_(double x, double* s, double* c) {
+#if IKG_CW_SINCOS
+    cw_sincos(x, s, c);
+#else
+    ::sincos(x, s, c);
+#endif
+  }
 };
 
 template <>
@@ -228,7 +308,13 @@ struct Prec<float> {
   static constexpr float kPrec3 = 0.1f;
   static constexpr float kPi = 3.14159265358979323846f;
   static constexpr float kRcond = 1e-7f;
-  IKG_HD static inline void sincos_(float x, float* s, float* c) { ::sincosf(x, s, c); }
+  IKG_HD static inline void sincos_(float x, float* s, float* c) {
+#if IKG_CW_SINCOS
+    cw_sincos(x, s, c);
+#else
+    ::sincosf(x, s, c);
+#endif
+  }
 };
 
 template <>
@@ -237,11 +323,26 @@ struct Prec<v2f> {
   static constexpr float kPi = Prec<float>::kPi;
   static constexpr float kRcond = Prec<float>::kRcond;
   IKG_HD static inline void sincos_(v2f x, v2f* s, v2f* c) {
+#if IKG_CW_SINCOS
+    // both halves' reductions and polynomials in packed math, quadrants per half
+    const v2f n = v2f{rintf(x.x * 0.636619772f), rintf(x.y * 0.636619772f)};
+    v2f r = x - n * 1.57079637f;  // contracted: fma(-n, C, x)
+    r = r - n * -4.37113883e-08f;
+    r = r - n * -1.71512489e-15f;
+    v2f sr, cr;
+    cw_poly(r, sr, cr);
+    float s0, c0, s1, c1;
+    cw_quadrant((int)n.x, sr.x, cr.x, &s0, &c0);
+    cw_quadrant((int)n.y, sr.y, cr.y, &s1, &c1);
+    *s = v2f{s0, s1};
+    *c = v2f{c0, c1};
+#else
     float s0, c0, s1, c1;
     ::sincosf(x.x, &s0, &c0);
     ::sincosf(x.y, &s1, &c1);
     *s = v2f{s0, s1};
     *c = v2f{c0, c1};
+#endif
   }
 };
 
