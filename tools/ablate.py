@@ -46,7 +46,7 @@ prm = _lib.Params(eps=float(os.environ.get("ABL_EPS", "1e-37")), dt=1e-2, max_it
                   variant=int(os.environ.get("ABL_VARIANT", "0")), lambda_=0.0)
 s = torch.cuda.current_stream().cuda_stream
 times = {n: [] for n, _, _ in handles}
-for rnd in range(6):
+for rnd in range(int(os.environ.get("ABL_ROUNDS", "6"))):
     for n, lib, h in handles:
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
