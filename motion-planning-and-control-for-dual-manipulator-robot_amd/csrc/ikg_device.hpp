@@ -216,6 +216,12 @@ IKG_HD inline v2f atan2f(v2f y, v2f x) { return atan2(y, x); }
 #ifndef IKG_CW_SINCOS
 #define IKG_CW_SINCOS 1
 #endif
+// the packed pair keeps OCML's sincosf: in packed math the polynomial version
+// measured 4% slower at C3 (fp32, q = 0; its exact trig runs at resyncs only)
+// and 3% faster with random seeds (large steps) -- interleaved A/B, same build
+#ifndef IKG_CW_SINCOS_PACKED
+#define IKG_CW_SINCOS_PACKED 0
+#endif
 template <typename T>
 IKG_HD inline void cw_poly(T r, T& sr, T& cr) {
   const T r2 = r * r;
@@ -323,7 +329,7 @@ struct Prec<v2f> {
   static constexpr float kPi = Prec<float>::kPi;
   static constexpr float kRcond = Prec<float>::kRcond;
   IKG_HD static inline void sincos_(v2f x, v2f* s, v2f* c) {
-#if IKG_CW_SINCOS
+#if IKG_CW_SINCOS && IKG_CW_SINCOS_PACKED
     // both halves' reductions and polynomials in packed math, quadrants per half
     const v2f n = v2f{rintf(x.x * 0.636619772f), rintf(x.y * 0.636619772f)};
     v2f r = x - n * 1.57079637f;  // contracted: fma(-n, C, x)
@@ -401,7 +407,11 @@ IKG_HD inline T frcp(T b) {
 }
 
 // sqrt(x) for 0 <= x <= 4 (|skew| of a rotation): OCML's refinement without
-// its denormal scaling and special-value selects (x = 0 gives 0)
+// its denormal scaling and special-value selects (x = 0 gives 0); fp32: the
+// hardware v_sqrt_f32 (IKG_RAW_SQRTF=0: OCML's sqrtf)
+#ifndef IKG_RAW_SQRTF
+#define IKG_RAW_SQRTF 1
+#endif
 template <typename T>
 IKG_HD inline T fsqrt_unit(T x) {
 #ifdef __HIP_DEVICE_COMPILE__
@@ -414,8 +424,13 @@ IKG_HD inline T fsqrt_unit(T x) {
     // one correction already rounds correctly (tools/ubench/rcp.hip)
     const double d = fma(-g, g, x);
     return fma(d, h, g);
-  } else {
+  } else if constexpr (!IKG_RAW_SQRTF) {
     return sqrt(x);
+  } else if constexpr (is_packed<T>) {
+    // v_sqrt_f32 (1 ulp) without OCML's denormal scaling and class checks
+    return T{__builtin_amdgcn_sqrtf(x.x), __builtin_amdgcn_sqrtf(x.y)};
+  } else {
+    return __builtin_amdgcn_sqrtf(x);
   }
 #else
   if constexpr (is_packed<T>)

@@ -1,14 +1,18 @@
 #!/bin/bash
 # Timing-only variant builds of the kernel library (tools/ablate.py times them
-# interleaved in one process).  usage: tools/build_variants.sh name "extra flags" [name "flags"]...
+# interleaved in one process), built by the Makefile with the shipped per-file
+# flags (the packed kernel's max-ILP scheduler) plus the variant's flags, into
+# ikgrasp/_native/var/lib_<name>.so.
+# usage: tools/build_variants.sh name "extra flags" [name "flags"]...
 set -e
 cd "$(dirname "$0")/../motion-planning-and-control-for-dual-manipulator-robot_amd/csrc"
 mkdir -p ../ikgrasp/_native/var
 rm -f ../ikgrasp/_native/var/*.so
+make -s build/ikg_jit_src.inc
 while [ $# -gt 0 ]; do
   name=$1; flags=$2; shift 2
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-slp-vectorize -Xarch_device -ffinite-math-only -Xarch_device -fno-signed-zeros -Xarch_device -Wno-nan-infinity-disabled $flags -I../../include -I. \
-    -shared -o ../ikgrasp/_native/var/lib_$name.so ikg_kernels.hip ikg_packed.hip ikg_quad.hip ikg_collision.hip ikg_control.hip ikg_jit.hip ikg_capi.hip -ldl &
+  make -s -j8 BUILD=build_var_$name EXTRA="$flags" OUT=../ikgrasp/_native/var/lib_$name.so ../ikgrasp/_native/var/lib_$name.so &
 done
 wait
+rm -rf build_var_*
 ls ../ikgrasp/_native/var
