@@ -216,9 +216,10 @@ IKG_HD inline v2f atan2f(v2f y, v2f x) { return atan2(y, x); }
 #ifndef IKG_CW_SINCOS
 #define IKG_CW_SINCOS 1
 #endif
-// the packed pair keeps OCML's sincosf: in packed math the polynomial version
-// measured 4% slower at C3 (fp32, q = 0; its exact trig runs at resyncs only)
-// and 3% faster with random seeds (large steps) -- interleaved A/B, same build
+// The packed pair keeps OCML's sincosf (0).  The polynomial in packed math (1)
+// or per half (2) measured 4% slower at C3 (fp32, q = 0; its exact trig runs
+// at resyncs only), and (1) 3% faster with random seeds (large steps)
+// (profiles/r02/fp32_math_ab.txt, interleaved A/B of same-flag builds).
 #ifndef IKG_CW_SINCOS_PACKED
 #define IKG_CW_SINCOS_PACKED 0
 #endif
@@ -329,7 +330,7 @@ struct Prec<v2f> {
   static constexpr float kPi = Prec<float>::kPi;
   static constexpr float kRcond = Prec<float>::kRcond;
   IKG_HD static inline void sincos_(v2f x, v2f* s, v2f* c) {
-#if IKG_CW_SINCOS && IKG_CW_SINCOS_PACKED
+#if IKG_CW_SINCOS && IKG_CW_SINCOS_PACKED == 1
     // both halves' reductions and polynomials in packed math, quadrants per half
     const v2f n = v2f{rintf(x.x * 0.636619772f), rintf(x.y * 0.636619772f)};
     v2f r = x - n * 1.57079637f;  // contracted: fma(-n, C, x)
@@ -340,6 +341,12 @@ struct Prec<v2f> {
     float s0, c0, s1, c1;
     cw_quadrant((int)n.x, sr.x, cr.x, &s0, &c0);
     cw_quadrant((int)n.y, sr.y, cr.y, &s1, &c1);
+    *s = v2f{s0, s1};
+    *c = v2f{c0, c1};
+#elif IKG_CW_SINCOS && IKG_CW_SINCOS_PACKED == 2
+    float s0, c0, s1, c1;  // the scalar polynomial per half
+    cw_sincos(x.x, &s0, &c0);
+    cw_sincos(x.y, &s1, &c1);
     *s = v2f{s0, s1};
     *c = v2f{c0, c1};
 #else
