@@ -176,3 +176,20 @@ def test_specialising_compile_cache(tmp_path, monkeypatch):
     assert (tmp_path / "a.co").read_bytes() == (tmp_path / "b.co").read_bytes()
     a.close()
     b.close()
+
+
+def test_specialising_compile_cache_ignores_damaged_files(tmp_path, monkeypatch):
+    """A cache file that is not an ELF code object is recompiled and replaced."""
+    from ikgrasp.solver import IKSolver
+    monkeypatch.setenv("IKG_JIT_CACHE_DIR", str(tmp_path))
+    n = C.c_size_t()
+    a = IKSolver()
+    assert a.lib.ikg_debug_jit_compile(a._h, _lib.IKG_F32, None, C.byref(n)) == 0
+    (f,) = list(tmp_path.glob("ikg_jit_*.co"))
+    good = f.read_bytes()
+    f.write_bytes(b"not a code object")
+    b = IKSolver()
+    assert b.lib.ikg_debug_jit_compile(b._h, _lib.IKG_F32, None, C.byref(n)) == 0
+    assert n.value == len(good) and f.read_bytes() == good
+    a.close()
+    b.close()
