@@ -67,8 +67,15 @@ def cpu_baseline(targets, budget_s=10.0):
     t0 = time.perf_counter()
     _, conv, iters, _ = c_oracle.solve(sample, np.zeros(15), threads=threads)
     dt = time.perf_counter() - t0
+    cpu_model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
+    except OSError:
+        pass
     return {
         "value": float(conv.sum() / dt), "unit": "converged solves/s", "cores": threads, "kind": "port",
+        "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
         "sample": f"{n} solves = the {len(targets)} benchmark targets x {n / len(targets):.2f}, q0=0, fp64 C "
                   f"restatement (oracle/ikg_oracle.c, OpenMP), {dt:.1f} s; all-problem rate {n / dt:.1f}/s",
     }
