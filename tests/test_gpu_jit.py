@@ -175,3 +175,39 @@ def test_ragged_batches(tilted_pair, gc):
         a = jit.solve(gc["targets"][:B], gc["q0"][:B])
         b = pre.solve(gc["targets"][:B], gc["q0"][:B])
         _same(a, b)
+
+
+def _tilted_scene(model):
+    """The tilted robot's URDF collision primitives plus a world-fixed table box
+    and the grasp cube (a 0.1 m box at each solve's target); every pair of
+    geometries on different joints."""
+    import xml.etree.ElementTree as ET
+
+    from ikgrasp.collision import BOX, CollisionScene, Geom, _link_geoms, _robot_link_frames
+    root = ET.parse(os.path.join(GOLDEN, "tilted_dualarm.urdf")).getroot()
+    geoms = _link_geoms(root, _robot_link_frames(root, model.joint_names, model.axis_frames()))
+    geoms.append(Geom("table_0", BOX, -1, "table", np.eye(3), np.array([0.6, 0.0, 0.55]),
+                      np.array([0.3, 0.6, 0.05])))
+    geoms.append(Geom("cube_0", BOX, -1, "cube", np.eye(3), np.zeros(3), np.array([0.05, 0.05, 0.05]), True))
+    n = len(geoms)
+    pairs = [(i, j) for i in range(n) for j in range(i + 1, n) if geoms[i].joint != geoms[j].joint]
+    return CollisionScene(geoms, np.array(pairs, dtype=np.int32))
+
+
+def test_tilted_collision_term_specialised_vs_prebuilt(gc):
+    """check_collision on a generic model: the specialised batch kernel followed
+    by the (prebuilt, generic-table) collision continuation gives the prebuilt
+    path's flags and update counts; successful solves are collision-free."""
+    from ikgrasp.solver import IKSolver
+    m = _tilted_model()
+    scene = _tilted_scene(m)
+    jit, pre = IKSolver(m, device=0, scene=scene), IKSolver(m, device=0, scene=scene, specialize=False)
+    a = jit.solve(gc["targets"], gc["q0"], check_collision=True)
+    assert jit.is_specialized("f64")
+    b = pre.solve(gc["targets"], gc["q0"], check_collision=True)
+    _same(a, b, tol=1e-9)
+    ok = a.converged.astype(bool)
+    assert ok.any()
+    assert not jit.collision(a.q[ok], gc["targets"][ok]).any()
+    jit.close()
+    pre.close()
