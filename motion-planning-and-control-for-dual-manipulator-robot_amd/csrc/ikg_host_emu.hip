@@ -229,3 +229,40 @@ extern "C" int ikg_emu_epa(int kindA, const double* RA, const double* tA, const 
   *depth = epa_depth_lb(A, B, pts, s);
   return 0;
 }
+
+// The loop's math helpers over arrays (tests/test_host_emu.py accuracy checks):
+// fn 0: cw_sincos (fp64), 1: cw_sincos (fp32), 2: the packed pair's sincos
+// (both halves), 3: atan2_upper (fp32), 4: atan2_upper (packed pair).
+// out holds 2 values per input (sin, cos) for fn 0-2, 1 for fn 3-4.
+extern "C" int ikg_emu_math(int fn, int64_t n, const double* x, const double* y, double* out) {
+  using namespace ikg;
+  for (int64_t i = 0; i < n; ++i) {
+    switch (fn) {
+      case 0: cw_sincos(x[i], &out[2 * i], &out[2 * i + 1]); break;
+      case 1: {
+        float s, c;
+        cw_sincos((float)x[i], &s, &c);
+        out[2 * i] = s;
+        out[2 * i + 1] = c;
+        break;
+      }
+      case 2: {
+        v2f s, c;
+        Prec<v2f>::sincos_(v2f{(float)x[i], (float)-x[i]}, &s, &c);
+        out[2 * i] = s.x;
+        out[2 * i + 1] = c.x;
+        if (s.y != -s.x || c.y != c.x) return -2;  // the halves are independent and symmetric
+        break;
+      }
+      case 3: out[i] = atan2_upper((float)y[i], (float)x[i]); break;
+      case 4: {
+        const v2f r = atan2_upper(v2f{(float)y[i], (float)y[i]}, v2f{(float)x[i], (float)x[i]});
+        if (r.x != r.y) return -2;
+        out[i] = r.x;
+        break;
+      }
+      default: return -1;
+    }
+  }
+  return 0;
+}

@@ -97,3 +97,40 @@ def test_medium_trig_series_matches_exact_fallback(emu, dtype):
         b = emu(tg, seed, dtype=dtype, broadcast=True, max_iters=150)
         assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
         assert np.abs(a[0] - b[0]).max() <= (1e-10 if dtype == 0 else 1e-3)
+
+
+def _emu_math(fn, x, y=None):
+    lib = C.CDLL(EMU)
+    lib.ikg_emu_math.argtypes = [C.c_int, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p]
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(x if y is None else y, dtype=np.float64)
+    out = np.empty(2 * len(x), dtype=np.float64)
+    assert lib.ikg_emu_math(fn, len(x), x.ctypes.data, y.ctypes.data, out.ctypes.data) == 0
+    return out
+
+
+def test_loop_math_accuracy():
+    """The loop's own math (ikg_device.hpp): Cody-Waite sincos within 2 ulp
+    (fp64) / 2 ulp of float (fp32) over the joint range and beyond, and the
+    packed pair's atan2_upper within 1.5 float ulps of pi (3.6e-7) over the
+    upper half plane (host arithmetic: exact division instead of the device's
+    reciprocal refinement)."""
+    if not os.path.exists(EMU):
+        pytest.skip("libikgrasp_emu.so not built")
+    rng = np.random.default_rng(7)
+    x = np.concatenate([rng.uniform(-8, 8, 20000), np.linspace(-np.pi, np.pi, 4001), [0.0, 1e-300, -1e-300]])
+    o = _emu_math(0, x).reshape(-1, 2)
+    assert np.abs(o[:, 0] - np.sin(x)).max() <= 2 * np.spacing(1.0)
+    assert np.abs(o[:, 1] - np.cos(x)).max() <= 2 * np.spacing(1.0)
+    xf = x.astype(np.float32).astype(np.float64)
+    for fn in (1, 2):
+        o = _emu_math(fn, xf).reshape(-1, 2)
+        assert np.abs(o[:, 0] - np.sin(xf)).max() <= 2 * float(np.spacing(np.float32(1.0)))
+        assert np.abs(o[:, 1] - np.cos(xf)).max() <= 2 * float(np.spacing(np.float32(1.0)))
+    th = np.concatenate([rng.uniform(0, np.pi, 20000), [0.0, np.pi / 4, np.pi / 2, np.pi, 1e-6, np.pi - 1e-6]])
+    r = rng.uniform(0.5, 2.0, len(th))
+    yy = (r * np.sin(th)).astype(np.float32).astype(np.float64)
+    xx = (r * np.cos(th)).astype(np.float32).astype(np.float64)
+    for fn in (3, 4):
+        a = _emu_math(fn, xx, yy)[:len(xx)]
+        assert np.abs(a - np.arctan2(yy, xx)).max() <= 1.5 * float(np.spacing(np.float32(np.pi)))
