@@ -81,6 +81,47 @@ def cpu_baseline(targets, budget_s=10.0):
     }
 
 
+class QGather:
+    """The per-step gather of the final q to rank 0 (north star: "at most an
+    RCCL gather of the final q over xGMI").  Device collectives (RCCL): step
+    k's gather runs asynchronously on the communicator's stream while step k+1
+    solves into the other q buffer; a buffer is handed out again only after
+    its gather has been waited on (for RCCL a stream wait, not a host block).
+    Host collectives (the gloo rehearsal): synchronous gathers of host copies."""
+
+    def __init__(self, dist, q_out, gathered, world, enabled=True, host=False):
+        self.dist, self.gathered, self.host = dist, gathered, host
+        self.on = world > 1 and enabled
+        self.overlap = self.on and not host
+        self.bufs = [q_out, q_out.new_empty(q_out.shape)] if self.overlap else [q_out]
+        self.pending = [None] * len(self.bufs)
+        self.k = 0
+
+    def buffer(self):
+        i = self.k % len(self.bufs)
+        if self.pending[i] is not None:
+            self.pending[i].wait()
+            self.pending[i] = None
+        return self.bufs[i]
+
+    def submit(self, qb):
+        i = self.k % len(self.bufs)
+        assert qb is self.bufs[i]
+        self.k += 1
+        if not self.on:
+            return
+        if self.overlap:
+            self.pending[i] = self.dist.gather(qb, self.gathered, dst=0, async_op=True)
+        else:
+            self.dist.gather(qb.cpu() if qb.device.type != "cpu" else qb, self.gathered, dst=0)
+
+    def drain(self):
+        for i, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[i] = None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -152,22 +193,25 @@ def main():
         seeds = torch.tensor(seeds_np, dtype=tdt, device=dev)
         best = torch.empty(B, dtype=torch.int32, device=dev)
 
+    gather = QGather(dist, q_out, gathered, world, enabled=not args.no_gather, host=host)
+
     def step(ev=None):
+        qb = gather.buffer()
         if ev is not None:
             ev[0].record(stream)
         if S:
-            solver.solve_multistart_into(targets, seeds, q_out, conv, iters, err, best, code, sh,
+            solver.solve_multistart_into(targets, seeds, qb, conv, iters, err, best, code, sh,
                                          variant=args.variant, check_collision=args.collision)
         else:
-            solver.solve_into(targets, q0, q_out, conv, iters, err, code, sh, variant=args.variant,
+            solver.solve_into(targets, q0, qb, conv, iters, err, code, sh, variant=args.variant,
                               check_collision=args.collision)
         if ev is not None:
             ev[1].record(stream)
-        if world > 1 and not args.no_gather:
-            dist.gather(q_out.cpu() if host else q_out, gathered, dst=0)
+        gather.submit(qb)
 
     for _ in range(args.warmup):
         step()
+    gather.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -176,6 +220,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(events[k])
+    gather.drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
