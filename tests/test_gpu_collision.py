@@ -67,15 +67,22 @@ def test_collision_batch_large_is_consistent(csolver, col_cases):
     assert np.array_equal(got, base)
 
 
-# continuation schedule: the default, certified stretches run inside
-# the continuation kernel (0 rounds), handed to ikg_cert_stretch_kernel (2)
+# continuation schedule: the default (trajectory first: ikg_traj_kernel's
+# recorded iterates scanned by ikg_traj_scan_kernel), and the interleaved
+# continuation (IKG_CONT_TRAJ=0) with its certified stretches inside the
+# continuation kernel (0 rounds) or handed to ikg_cert_stretch_kernel (2)
 ROUNDS = [None, "0", "2"]
+
+
+def _schedule(monkeypatch, rounds):
+    if rounds is not None:
+        monkeypatch.setenv("IKG_CONT_TRAJ", "0")
+        monkeypatch.setenv("IKG_HANDOFF_ROUNDS", rounds)
 
 
 @pytest.mark.parametrize("rounds", ROUNDS)
 def test_solve_with_collision_fp64(csolver, solve_cases, oracle_cases, rounds, monkeypatch):
-    if rounds is not None:
-        monkeypatch.setenv("IKG_HANDOFF_ROUNDS", rounds)
+    _schedule(monkeypatch, rounds)
     c = solve_cases
     sol = csolver.solve(c["targets"], c["q0"], check_collision=True)
     assert np.array_equal(sol.converged, c["success"])
@@ -93,8 +100,7 @@ def test_solve_with_collision_fp64(csolver, solve_cases, oracle_cases, rounds, m
 
 @pytest.mark.parametrize("rounds", ROUNDS)
 def test_solve_with_collision_fp32(csolver, solve_cases, rounds, monkeypatch):
-    if rounds is not None:
-        monkeypatch.setenv("IKG_HANDOFF_ROUNDS", rounds)
+    _schedule(monkeypatch, rounds)
     c = solve_cases
     sol = csolver.solve(c["targets"], c["q0"], dtype="f32", check_collision=True)
     agree = (sol.converged == c["success"]).mean()
@@ -174,3 +180,36 @@ def test_solve_with_collision_small_and_empty_batches(csolver, solve_cases):
         one = csolver.solve(c["targets"][i:i + 1], c["q0"][i:i + 1], check_collision=True)
         assert one.converged[0] == full.converged[i] and one.iters[0] == full.iters[i]
         assert np.abs(one.q[0] - full.q[i]).max() <= 1e-12
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_trajectory_continuation_equals_interleaved(csolver, dtype, monkeypatch):
+    """The trajectory-first continuation (default) and the interleaved one
+    answer the same question -- the first iterate whose errors pass without
+    collision -- on the same iterates: at C2's 4,096 uniform-sampler targets
+    the flags and update counts agree (fp64: all; fp32: 99%) and q agrees to
+    the rounding of the two FK formulations the iterates were computed with."""
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(4096, seed=0)
+    a = csolver.solve(tg, np.zeros(15), dtype=dtype, check_collision=True)
+    monkeypatch.setenv("IKG_CONT_TRAJ", "0")
+    b = csolver.solve(tg, np.zeros(15), dtype=dtype, check_collision=True)
+    same = (a.converged == b.converged) & (a.iters == b.iters)
+    if dtype == "f64":
+        assert same.all()
+        assert np.abs(a.q - b.q).max() <= 1e-9
+    else:
+        assert same.mean() >= 0.99
+        assert np.abs(a.q[same] - b.q[same]).max() <= 1e-3
+
+
+def test_trajectory_continuation_windows(csolver, solve_cases, monkeypatch):
+    """Windows shorter than the loop (several update/scan rounds, certificates
+    carried across them) give the single-window answer: IKG_TRAJ_WINDOW forces
+    16-iterate windows."""
+    c = solve_cases
+    a = csolver.solve(c["targets"], c["q0"], check_collision=True)
+    monkeypatch.setenv("IKG_TRAJ_WINDOW", "16")
+    b = csolver.solve(c["targets"], c["q0"], check_collision=True)
+    assert np.array_equal(a.converged, b.converged) and np.array_equal(a.iters, b.iters)
+    assert np.abs(a.q - b.q).max() <= 1e-12
