@@ -18,6 +18,10 @@ for d, name in [("prof_f64", "kernel_stats_b4096_f64.csv"), ("prof_f32", "kernel
     hits = glob.glob(os.path.join(src, d, "**", "*kernel_stats.csv"), recursive=True)
     if hits:
         shutil.copy(hits[0], os.path.join(dst, name))
+hits = glob.glob(os.path.join(src, "prof_col_c2", "**", "*kernel_stats.csv"), recursive=True)
+if hits:
+    os.makedirs(os.path.join(dst, "collision"), exist_ok=True)
+    shutil.copy(hits[0], os.path.join(dst, "collision", "kernel_stats_c2_f64.csv"))
 for sub in ["collision", "matrix"]:
     os.makedirs(os.path.join(dst, sub), exist_ok=True)
     for f in glob.glob(os.path.join(src, sub, "*.json")):

@@ -25,6 +25,15 @@ run() { d=$1; n=$2; shift 2; timeout -k 10 240 python bench.py "$@" > $O/$d/$n.j
 run collision c2_f64 --collision --no-cpu-baseline
 run collision c3_f32 --collision --dtype f32 --batch 65536 --no-cpu-baseline
 run collision c5_f32 --collision --dtype f32 --batch 512 --multistart 256 --no-cpu-baseline
+run collision c5_f64 --collision --dtype f64 --batch 512 --multistart 256 --no-cpu-baseline
+run collision c4share_f64 --collision --dtype f64 --batch 131072 --no-cpu-baseline
+run collision c4share_f32 --collision --dtype f32 --batch 131072 --no-cpu-baseline
+IKG_CONT_TRAJ=0 timeout -k 10 240 python bench.py --collision --no-cpu-baseline > $O/collision/c2_f64_interleaved.json 2>> $O/bench.err; fatal $? c2i
+IKG_CONT_TRAJ=0 timeout -k 10 240 python bench.py --collision --dtype f32 --batch 65536 --no-cpu-baseline > $O/collision/c3_f32_interleaved.json 2>> $O/bench.err; fatal $? c3i
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_col_c2 -o run -- \
+  python3 $ROOT/bench.py --collision --steps 10 --warmup 2 --no-cpu-baseline > $O/prof_col_c2.json 2>> $O/bench.err; fatal $? profcol
+cd $ROOT
 run matrix c2_yaw_b4096_f64 --yaw 0.785398 --no-cpu-baseline
 run matrix c3_b65536_f64 --dtype f64 --batch 65536 --no-cpu-baseline
 run matrix c4share_b131072_f64 --dtype f64 --batch 131072 --no-cpu-baseline
