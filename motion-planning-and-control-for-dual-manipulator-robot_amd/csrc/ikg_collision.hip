@@ -1839,10 +1839,13 @@ template <typename T, bool DAMPED, class SP>
 static void launch_continue_sel(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
                                 const BatchArgs& a, int nq, int ng, const ContWs<T>& w, hipStream_t s,
                                 hipError_t& err, bool first) {
-  if (cont_traj(a.B))
+  if (cont_traj(a.B)) {
     err = launch_traj_t<T, DAMPED, SP>(dm, dc, prm, a, nq, w, first, s);
-  else
-    launch_continue_t<T, DAMPED, SP>(dm, dc, prm, a, nq, ng, w, s);
+    if (err != hipErrorOutOfMemory || first) return;
+    (void)hipGetLastError();  // no room for the record buffers: the interleaved continuation needs none
+    err = hipSuccess;
+  }
+  launch_continue_t<T, DAMPED, SP>(dm, dc, prm, a, nq, ng, w, s);
 }
 
 template <typename T>
