@@ -1301,7 +1301,7 @@ struct TrajCert {  // a problem's witness pair between windows
 // updates run in the same launch as window r's scan.
 template <typename T>
 struct TrajWs {
-  T* rec;             // [parity][slot][Wn][nq + 3]: q, |e_L|, |e_R|, stop test passes (1/0)
+  T* rec;             // [parity][slot][Wn][rec_len]: q, squared hand errors, stop test (see below)
   T* qrun;            // [slot][nq]: the iterate the next window starts from
   int32_t* itrun;     // its update count
   int32_t* it0;       // [parity][slot]: update count of the window's first record
@@ -1311,10 +1311,26 @@ struct TrajWs {
   int64_t slots;      // slots per parity
 };
 constexpr int32_t kTrajEnded = 1 << 30;
-// record slots: root, left arm joints, right arm joints, passive joints (in
-// passive_q order), then |e_L|, |e_R|, stop test (q-index order through
-// rec_slots, so each lane stores its arm at immediate offsets)
-constexpr int kRecRoot = 0, kRecArm0 = 1, kRecArm1 = 1 + kArmDof, kRecPassive = 1 + 2 * kArmDof;
+// Record layout: one 8-value block per arm lane, each written by four
+// 16-byte stores (fp64; two for fp32):
+//   [0, 8):  root, left arm joints 0..5, |e_L|^2
+//   [8, 16): stop test passes (1/0), right arm joints 0..5, |e_R|^2
+//   [16, ...): passive joints (passive_q order), padded to a multiple of 4
+// rec_slots maps q indices to slots.
+constexpr int kRecRoot = 0, kRecArm0 = 1, kRecErr0 = 7, kRecPass = 8, kRecArm1 = 9, kRecErr1 = 15, kRecPassive = 16;
+__host__ __device__ inline int rec_len(int n_passive) { return kRecPassive + ((n_passive + 3) & ~3); }
+
+template <typename T>
+__device__ __forceinline__ void store_block8(T* dst, const T (&v)[8]) {
+  if constexpr (sizeof(T) == 8) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) reinterpret_cast<double2*>(dst)[k] = make_double2(v[2 * k], v[2 * k + 1]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      reinterpret_cast<float4*>(dst)[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+  }
+}
 
 template <typename T>
 __device__ inline void rec_slots(const KModel<T>* __restrict__ m, int lane, int32_t* sl) {
@@ -1336,14 +1352,14 @@ __device__ __forceinline__ void traj_window(const KModel<T>* __restrict__ m, con
   // full waves: a wave with few live lanes issues the same loop up to 2.5x
   // slower (Live lanes)
   constexpr int ppw = 32;
-  const int nq = m->nq, RL = nq + 3;
+  const int nq = m->nq, RL = rec_len(m->n_passive);
   const int64_t par = (int64_t)(round & 1) * w.slots;
   for (int base = blk * ppw; base < n; base += nb * ppw) {
     const int i = base + (lane >> 1);
     if (lane >= 2 * ppw || i >= n) continue;  // both lanes of a pair together
     // answered, or its loop already exhausted (the scan of that window, running
     // beside this one, answers it); `done` may be stale here: extra work only
-    if (w.done[i] || (round > 0 && w.itrun[i] >= prm.max_iters)) continue;
+    if (round > 0 && (w.done[i] || w.itrun[i] >= prm.max_iters)) continue;
     const int64_t p = clist[i];
     const int64_t tgt = S_per_target > 1 ? p / S_per_target : p;
     T RT[9], tT[3], qc, qa[kArmDof], sn[7], cs[7];
@@ -1380,16 +1396,16 @@ __device__ __forceinline__ void traj_window(const KModel<T>* __restrict__ m, con
                                               j == 0 || (it % Trig<T>::kResync) == 0);
       const T xo = pair_swap(x);
       ended = it >= prm.max_iters;
-      T* r = rec + (int64_t)j * RL;
-      if (arm == 0) {
-        r[kRecRoot] = qc;
+      {
         // the iterate after max_iters is never tested (:56 loop exhausted)
-        r[nq + 2] = (!ended && x < prm.eps2 && xo < prm.eps2) ? T(1) : T(0);
-      }
-      T* ra = r + (arm ? kRecArm1 : kRecArm0);  // immediate offsets from one address
+        const T pass = (!ended && x < prm.eps2 && xo < prm.eps2) ? T(1) : T(0);
+        T blk[8];
+        blk[0] = arm ? pass : qc;
 #pragma unroll
-      for (int k = 0; k < kArmDof; ++k) ra[k] = qa[k];
-      r[nq + arm] = sqrt(x);
+        for (int k = 0; k < kArmDof; ++k) blk[1 + k] = qa[k];
+        blk[7] = x;  // squared: the scan takes the root of the answer's only
+        store_block8(rec + (int64_t)j * RL + (arm ? kRecPass : kRecRoot), blk);
+      }
       ++j;
       if (ended) break;
       stretch_update<T, DAMPED, SP>(m, prm, arm, s, dq, it, qc, qa, sn, cs, lim);
@@ -1483,7 +1499,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
   __shared__ T PL[64][2][12];  // per-lane witness placements
   __shared__ int32_t SL[kMaxNq];  // joint -> record slot
   const int lane = threadIdx.x;
-  const int nq = m->nq, RL = nq + 3;
+  const int nq = m->nq, RL = rec_len(m->n_passive);
   const int64_t par = (int64_t)(round & 1) * w.slots;
   rec_slots(m, lane, SL);
   for (int i = blk; i < n; i += nb) {
@@ -1526,7 +1542,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     for (int start = 0; start < nrec && ans < 0; start += 64) {
       const int j = start + lane;
       const T* r = rec + (int64_t)min(j, nrec - 1) * RL;
-      bool need = j < nrec && r[nq + 2] != T(0);
+      bool need = j < nrec && r[kRecPass] != T(0);
       while (__any(need)) {
         const int wp = W.pair;
         const bool hit = need && wp >= 0 && witness_hit_lane(m, c, wp, r, SL, tgt, PL[lane]);
@@ -1569,7 +1585,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     if (a >= 0) {  // final: the answer, or the iterate after max_iters (success = False)
       const T* r = rec + (int64_t)a * RL;
       if (lane < nq) q_out[p * nq + lane] = r[SL[lane]];
-      if (lane < 2) err[p * 2 + lane] = r[nq + lane];
+      if (lane < 2) err[p * 2 + lane] = sqrt(r[lane ? kRecErr1 : kRecErr0]);
       if (lane == 0) {
         conv[p] = ans >= 0 ? 1 : 0;
         iters[p] = w.it0[par + i] + a;
@@ -1764,7 +1780,8 @@ __global__ __launch_bounds__(256) void ikg_fill_i32_kernel(int32_t* __restrict__
 template <typename T, bool DAMPED, class SP>
 static hipError_t launch_traj_t(const KModel<T>* dm, const KCollision<T>* dc, const KParams<T>& prm,
                                 const BatchArgs& a, int nq, const ContWs<T>& cw, bool first, hipStream_t s) {
-  const size_t RL = (size_t)nq + 3, B = (size_t)a.B;
+  // every joint is the root, an arm joint or passive (ikg_model_build.hpp)
+  const size_t RL = (size_t)rec_len(std::max(0, nq - 1 - 2 * kArmDof)), B = (size_t)a.B;
   const size_t full = (size_t)prm.max_iters + 1;
   const size_t per = 2 * RL * sizeof(T) * B;  // one iterate of every slot, both buffers
   int Wn = (int)std::min({full, (size_t)kTrajWindow, std::max<size_t>(16, kTrajBudget / per)});

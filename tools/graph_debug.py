@@ -1,42 +1,48 @@
-"""Collision solve captured in a hipGraph: which problems differ between a
-replay on new targets and the direct solve (trajectory continuation)."""
+"""Collision solve captured in a hipGraph (the sequence of
+tests/test_gpu_graph.py), repeated: on a mismatch between a replay and the
+direct solve, print both and the pre-screen schedule's answer."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd"))
-import numpy as np
 import torch
 from ikgrasp import _lib
 from ikgrasp.collision import load_nextage_scene
 from ikgrasp.solver import IKSolver
 from ikgrasp.workload import uniform_targets
 dev = torch.device("cuda", 0)
-s = IKSolver(device=0, scene=load_nextage_scene())
+mode = os.environ.get("IKG_TRAJ_PRESCREEN", "1")
 def bufs():
     return (torch.empty((1024, 15), dtype=torch.float64, device=dev), torch.empty(1024, dtype=torch.uint8, device=dev),
             torch.empty(1024, dtype=torch.int32, device=dev), torch.empty((1024, 2), dtype=torch.float64, device=dev))
-def direct(tg):
-    b = bufs()
-    s.solve_into(tg, q0, *b, _lib.IKG_F64, torch.cuda.current_stream().cuda_stream, check_collision=True)
-    torch.cuda.synchronize()
-    return b
-tg = torch.tensor(uniform_targets(1024, seed=3), dtype=torch.float64, device=dev)
-q0 = torch.zeros(15, dtype=torch.float64, device=dev)
-out = bufs()
-g = torch.cuda.CUDAGraph()
-side = torch.cuda.Stream(); side.wait_stream(torch.cuda.current_stream())
-with torch.cuda.stream(side):
-    s.solve_into(tg, q0, *out, _lib.IKG_F64, side.cuda_stream, check_collision=True)
-torch.cuda.current_stream().wait_stream(side); torch.cuda.synchronize()
-with torch.cuda.graph(g):
-    s.solve_into(tg, q0, *out, _lib.IKG_F64, torch.cuda.current_stream().cuda_stream, check_collision=True)
-for seed in (3, 4, 3, 4):
-    tg.copy_(torch.tensor(uniform_targets(1024, seed=seed), dtype=torch.float64, device=dev))
+for rep in range(4):
+    s = IKSolver(device=0, scene=load_nextage_scene())
+    q0 = torch.zeros(15, dtype=torch.float64, device=dev)
+    tg = torch.tensor(uniform_targets(1024, seed=3), dtype=torch.float64, device=dev)
+    def direct(pre=None):
+        if pre is not None: os.environ["IKG_TRAJ_PRESCREEN"] = pre
+        b = bufs()
+        s.solve_into(tg, q0, *b, _lib.IKG_F64, torch.cuda.current_stream().cuda_stream, check_collision=True)
+        torch.cuda.synchronize()
+        os.environ["IKG_TRAJ_PRESCREEN"] = mode
+        return b
+    ref = direct()
+    out = bufs()
+    side = torch.cuda.Stream(); side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        s.solve_into(tg, q0, *out, _lib.IKG_F64, side.cuda_stream, check_collision=True)
+    torch.cuda.current_stream().wait_stream(side); torch.cuda.synchronize()
     for x in out: x.zero_()
-    g.replay(); torch.cuda.synchronize()
-    ref = direct(tg)
-    ref_b = direct(tg)
-    dc = torch.nonzero(out[1] != ref[1]).flatten().tolist()
-    di = torch.nonzero(out[2] != ref[2]).flatten().tolist()
-    dd = torch.nonzero(ref_b[2] != ref[2]).flatten().tolist()
-    print("seed", seed, "conv replay/direct", int(out[1].sum()), int(ref[1].sum()), "flag diffs", len(dc), dc[:6],
-          "iter diffs", len(di), [(i, int(out[2][i]), int(ref[2][i])) for i in di[:6]], "direct-vs-direct iter diffs", len(dd))
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s.solve_into(tg, q0, *out, _lib.IKG_F64, torch.cuda.current_stream().cuda_stream, check_collision=True)
+    for seed in (3, 4, 5, 4):
+        tg.copy_(torch.tensor(uniform_targets(1024, seed=seed), dtype=torch.float64, device=dev))
+        for x in out: x.zero_()
+        g.replay(); torch.cuda.synchronize()
+        d = direct()
+        good = direct("1")
+        bad_r = torch.nonzero((out[2] != good[2]) | (out[1] != good[1])).flatten().tolist()
+        bad_d = torch.nonzero((d[2] != good[2]) | (d[1] != good[1])).flatten().tolist()
+        print(f"rep {rep} seed {seed}: replay wrong {len(bad_r)} {[(i, int(out[1][i]), int(out[2][i]), int(good[1][i]), int(good[2][i])) for i in bad_r[:4]]}; direct wrong {len(bad_d)} {[(i, int(d[1][i]), int(d[2][i])) for i in bad_d[:4]]}", flush=True)
+    del g
+    s.close()
