@@ -15,6 +15,7 @@
 
 #include "ikg_device.hpp"
 #include "ikg_jit.hpp"
+#include "ikg_solve.hpp"
 #include "ikg_launch.hpp"
 #include "ikg_model_build.hpp"
 #include "ikgrasp.h"
@@ -207,6 +208,18 @@ ikg::KParams<T> kparams(const ikg_params* p) {
   return ikg::make_kparams<T>(p);
 }
 
+// Records in the batch kernel for the collision continuation (IKG_TRAJ_REC=1;
+// by default the trajectory kernel recomputes the updates past the first
+// passing iterate).  Opt-in: like IKG_TRAJ_PRESCREEN=0, it showed graph
+// replays that differed from the direct solve in tests/test_gpu_graph.py
+// runs (not reproduced outside pytest).  Up to kRecBudget
+// bytes of records per solve.
+static bool rec_in_batch() {
+  const char* e = getenv("IKG_TRAJ_REC");
+  return e && atoi(e) != 0;
+}
+constexpr size_t kRecBudget = size_t(1) << 30;
+
 template <typename T>
 int solve_batch_t(ikg_model* model, int device, const void* targets, const void* q0, int64_t q0_stride, int64_t B,
                   const ikg_params* params, void* q_out, uint8_t* converged, int32_t* iters, void* err_out,
@@ -243,10 +256,36 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
     if (st.rc) return st.rc;
   }
   a.jit = model->jit_kernels<T>(device);
+  // collision term, pair layout, Nextage loop: the batch kernel itself records
+  // every iterate from the first passing one on, for the continuation's scan
+  // (ikg_collision.hip); the records take (max_iters + 1) x
+  // rec_len values per problem, offered up to kRecBudget
+  bool rec_used = false;
+  void* rec = nullptr;
+  if (dc && model->spec == ikg::kSpecNextage && !(params->lambda > 0) && !a.jit && a.q0_stride == 0 &&
+      rec_in_batch()) {
+    const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
+    const size_t b_rec = (sizeof(T) * rl * ((size_t)params->max_iters + 1) * (size_t)B + 255) & ~(size_t)255;
+    if (b_rec <= kRecBudget && hipMallocAsync(&rec, b_rec + sizeof(int32_t) * (size_t)B, s) == hipSuccess) {
+      a.rec = rec;
+      a.rec_n = (int32_t*)((char*)rec + b_rec);
+      a.rec_used = &rec_used;
+    } else {
+      rec = nullptr;
+      (void)hipGetLastError();
+    }
+  }
   hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, model->spec, s);
-  if (e != hipSuccess) return hip_fail(e, "ikg pair kernel launch");
+  if (e != hipSuccess) {
+    if (rec) (void)hipFreeAsync(rec, s);
+    return hip_fail(e, "ikg pair kernel launch");
+  }
   if (dc) {
     e = ikg::launch_collide_continue<T>(dm, dc, kparams<T>(params), a, model->spec, nq, model->c64.n_geoms, s);
+    if (rec) {
+      const hipError_t ef = hipFreeAsync(rec, s);
+      if (e == hipSuccess) e = ef;
+    }
     if (e != hipSuccess) return hip_fail(e, "ikg collision continuation launch");
   }
   if (host) {

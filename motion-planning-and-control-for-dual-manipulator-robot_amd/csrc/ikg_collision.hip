@@ -17,6 +17,7 @@
 #include "ikg_collision.hpp"
 #include "ikg_device.hpp"
 #include "ikg_launch.hpp"
+#include "ikg_solve.hpp"
 
 namespace ikg {
 
@@ -1309,28 +1310,9 @@ struct TrajWs {
   int32_t* done;      // answered
   TrajCert<T>* cst;
   int64_t slots;      // slots per parity
+  int by_p = 0;       // records, counts and it0 indexed by problem (the pair kernel's records)
 };
-constexpr int32_t kTrajEnded = 1 << 30;
-// Record layout: one 8-value block per arm lane, each written by four
-// 16-byte stores (fp64; two for fp32):
-//   [0, 8):  root, left arm joints 0..5, |e_L|^2
-//   [8, 16): stop test passes (1/0), right arm joints 0..5, |e_R|^2
-//   [16, ...): passive joints (passive_q order), padded to a multiple of 4
-// rec_slots maps q indices to slots.
-constexpr int kRecRoot = 0, kRecArm0 = 1, kRecErr0 = 7, kRecPass = 8, kRecArm1 = 9, kRecErr1 = 15, kRecPassive = 16;
-__host__ __device__ inline int rec_len(int n_passive) { return kRecPassive + ((n_passive + 3) & ~3); }
-
-template <typename T>
-__device__ __forceinline__ void store_block8(T* dst, const T (&v)[8]) {
-  if constexpr (sizeof(T) == 8) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) reinterpret_cast<double2*>(dst)[k] = make_double2(v[2 * k], v[2 * k + 1]);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      reinterpret_cast<float4*>(dst)[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
-  }
-}
+// the record layout (kRec*, rec_len, store_block8) is in ikg_solve.hpp
 
 template <typename T>
 __device__ inline void rec_slots(const KModel<T>* __restrict__ m, int lane, int32_t* sl) {
@@ -1527,10 +1509,21 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       __syncthreads();
       continue;
     }
-    const int nr = w.nrec[par + i];
+    const int64_t ix = w.by_p ? p : par + i;
+    const int nr = w.nrec[ix];
     const int nrec = nr & ~kTrajEnded;
     const bool ended = (nr & kTrajEnded) != 0;
-    const T* rec = w.rec + (par + i) * Wn * RL;
+    const int it0 = w.it0[ix];
+    T* rec = w.rec + ix * Wn * RL;
+    if (w.by_p) {  // the pair kernel records no passive joints: constant from the first update on
+      const T* qo = q_out + p * nq;
+      for (int j = lane; j < nrec; j += 64)
+        for (int k = 0; k < m->n_passive; ++k) {
+          const int pj = m->passive_q[k];
+          rec[(int64_t)j * RL + kRecPassive + k] = it0 + j > 0 ? clampq(qo[pj], m->lo[pj], m->hi[pj]) : qo[pj];
+        }
+      __syncthreads();
+    }
     int ans = -1;
 #ifdef IKG_CPROF
     unsigned long long sprof[4] = {0, 0, 0, 0}, n_chk = 0, n_lane = 0;
@@ -1588,7 +1581,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       if (lane < 2) err[p * 2 + lane] = sqrt(r[lane ? kRecErr1 : kRecErr0]);
       if (lane == 0) {
         conv[p] = ans >= 0 ? 1 : 0;
-        iters[p] = w.it0[par + i] + a;
+        iters[p] = it0 + a;
         w.done[i] = 1;
       }
     } else if (lane == 0) {  // the witness carries over to the next window
@@ -1879,7 +1872,7 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
               (T*)(ws + 3 * ib + 256)};
   // trajectory continuation without a pre-screen: the first checks run in its
   // first launch, so every converged problem is listed
-  const bool first = cont_traj(a.B) && !traj_prescreen(a.B);
+  const bool first = !(a.rec_used && *a.rec_used) && cont_traj(a.B) && !traj_prescreen(a.B);
   if (first)
     hipLaunchKernelGGL(ikg_mark_converged_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s,
                        (const uint8_t*)a.converged, a.B, w.wit);
@@ -1894,7 +1887,27 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
   }
   const bool damped = prm.lambda > T(0);
   hipError_t ec = hipSuccess;
-  if (spec == kSpecNextage) {
+  if (a.rec_used && *a.rec_used) {  // the pair kernel recorded every iterate from the first passing one
+    char* dws = nullptr;
+    e = hipMallocAsync((void**)&dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
+    if (e != hipSuccess) return e;
+    TrajWs<T> tw{};
+    tw.rec = (T*)a.rec;
+    tw.nrec = a.rec_n;
+    tw.it0 = a.iters;
+    tw.done = (int32_t*)dws;
+    tw.cst = (TrajCert<T>*)(dws + ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255));
+    tw.slots = a.B;
+    tw.by_p = 1;
+    hipLaunchKernelGGL(ikg_fill_i32_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s, tw.done, a.B, 0);
+    hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)std::min<int64_t>(1024, a.B)), dim3(64), 0, s, dm, dc,
+                       (const T*)a.targets, a.S, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
+                       (const int32_t*)w.wit, tw, prm.max_iters + 1, 0, (T*)a.q_out, a.converged, a.iters,
+                       (T*)a.err_out);
+    ec = hipGetLastError();
+    const hipError_t ef2 = hipFreeAsync(dws, s);
+    if (ec == hipSuccess) ec = ef2;
+  } else if (spec == kSpecNextage) {
     if (damped)
       launch_continue_sel<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, w, s, ec, first);
     else

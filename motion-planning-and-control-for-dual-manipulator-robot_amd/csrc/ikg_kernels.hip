@@ -38,7 +38,7 @@ namespace ikg {
 #ifndef IKG_WPE
 #define IKG_WPE 0
 #endif
-template <typename T, bool DAMPED, class SP, bool MED = false>
+template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
 __global__ __launch_bounds__(64)
 #if IKG_WPE
 __attribute__((amdgpu_waves_per_eu(1, IKG_WPE)))
@@ -49,12 +49,13 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             int64_t S, int ppw, T* __restrict__ q_out,
                                                             uint8_t* __restrict__ conv_out,
                                                             int32_t* __restrict__ iters_out,
-                                                            T* __restrict__ err_out) {
+                                                            T* __restrict__ err_out, T* __restrict__ rec = nullptr,
+                                                            int32_t* __restrict__ rec_n = nullptr) {
   // model tables stay in global memory: the compiler hoists them into
   // registers (staging them in LDS and re-reading per iteration measured 8%
   // slower)
-  pair_batch_body<T, DAMPED, SP, MED>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
-                                      err_out);
+  pair_batch_body<T, DAMPED, SP, MED, REC>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
+                                           err_out, rec, rec_n);
 }
 
 
@@ -195,6 +196,13 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
   // per-problem seeds (multi-start, or a q0 row per target): large first steps
   // are common, so the frame-1 loop takes the medium-range trig series
   if constexpr (kFrame1<SP> && !DAMPED) {
+    if (a.rec && a.S == 1 && a.q0_stride == 0) {  // collision continuation records (ikg_collision.hip)
+      hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, false, true>), grid, dim3(64), lds_pad_bytes(), s,
+                         dmodel, prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out,
+                         a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n);
+      if (a.rec_used) *a.rec_used = true;
+      return;
+    }
     if (a.S > 1 || a.q0_stride != 0) {
       hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, true>), grid, dim3(64), lds_pad_bytes(), s, dmodel,
                          prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out,

@@ -25,6 +25,12 @@ struct BatchArgs {
   int variant = 0; // ikg_variant
   // model-specialised pair kernels on this device (ikg_model_specialize), or null
   const JitKernels* jit = nullptr;
+  // collision continuation: record buffers offered to the pair kernel (records
+  // every iterate from the first passing one on, RecOut); `rec_used` is set
+  // when the launch took them
+  void* rec = nullptr;
+  int32_t* rec_n = nullptr;
+  bool* rec_used = nullptr;
 };
 
 struct MultiArgs {

@@ -34,6 +34,45 @@ __device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T
 }
 
 
+// ---- trajectory records (collision continuation, ikg_collision.hip §3b)
+// One 8-value block per arm lane, written by 16-byte stores:
+//   [0, 8):  root, left arm joints 0..5, |e_L|^2
+//   [8, 16): stop test passes (1/0), right arm joints 0..5, |e_R|^2
+//   [16, ...): passive joints (passive_q order), padded to a multiple of 4
+constexpr int kRecRoot = 0, kRecArm0 = 1, kRecErr0 = 7, kRecPass = 8, kRecArm1 = 9, kRecErr1 = 15, kRecPassive = 16;
+constexpr int32_t kTrajEnded = 1 << 30;  // record count flag: the last is the iterate after max_iters
+IKG_HD inline int rec_len(int n_passive) { return kRecPassive + ((n_passive + 3) & ~3); }
+
+template <typename T>
+__device__ __forceinline__ void store_block8(T* dst, const T (&v)[8]) {
+  struct alignas(16) V16 {
+    T x[16 / sizeof(T)];
+  };
+  constexpr int per = 16 / (int)sizeof(T);
+#pragma unroll
+  for (int k = 0; k < 8 / per; ++k) {
+    V16 b;
+#pragma unroll
+    for (int e = 0; e < per; ++e) b.x[e] = v[k * per + e];
+    reinterpret_cast<V16*>(dst)[k] = b;
+  }
+}
+
+// Record-in-batch outputs of one problem (ikg_pair_batch_kernel with REC):
+// the loop goes on past the first iterate whose errors pass, recording every
+// iterate for the collision scan; that iterate's outputs are stored when reached.
+template <typename T>
+struct RecOut {
+  T* rec;               // this problem's records, (max_iters + 1) x rec_len
+  int32_t* nrec;        // this problem's record count (| kTrajEnded)
+  const T* qrow;        // its q0 row (passive joints)
+  T* qo;                // its q_out row
+  uint8_t* conv;        // its outputs at the first passing iterate
+  int32_t* iters;
+  T* err;
+  int rl;               // rec_len
+};
+
 // Stop test of inverse_geometry.py:70 on squared norms (KParams::eps2):
 // pair layout = this lane's hand and the partner's; packed = both halves.
 template <typename T, typename E>
@@ -48,10 +87,13 @@ __device__ inline bool both_below(T x, T xo, E eps2) {
 // float: this lane owns one arm (pair layout, partner = lane ^ 1); T = v2f:
 // this lane owns both arms (packed layout).  Returns (through refs) the final
 // q of this lane, the update count and the hand error norms at the returned q.
-template <typename T, bool DAMPED, class SP, bool MED = false>
+template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
 __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
                                   const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
-                                  T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out) {
+                                  T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out,
+                                  const RecOut<T>* ro = nullptr) {
+  static_assert(!REC || !is_packed<T>, "records: pair layout only");
+  int k0 = -1;  // REC: the first iterate whose errors pass
   static_assert(!(DAMPED && is_packed<T>), "the packed layout implements lambda = 0 only");
   constexpr bool F1 = kFrame1<SP> && !DAMPED;  // frame-1 path, its own trig slots
   T sn[7], cs[7];
@@ -113,10 +155,34 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     }
     }
     xo = pair_swap(x);
-    if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
-    if (both_below(x, xo, prm.eps2)) {  // |e_L| < eps and |e_R| < eps (:70)
-      conv = true;
-      break;
+    if constexpr (REC) {
+      const bool ended = it >= prm.max_iters;  // never tested (:56 loop exhausted)
+      const bool pass = !ended && both_below(x, xo, prm.eps2);
+      if (pass && k0 < 0) {  // the answer unless it collides: stored now, the loop goes on
+        k0 = it;
+        conv = true;
+        store_q(m, arm, ro->qrow, it, qc, qa, ro->qo);
+        ro->err[arm] = sqrt(x);
+        if (arm == 0) {
+          *ro->conv = 1;
+          *ro->iters = it;
+        }
+      }
+      if (k0 >= 0) {
+        T blk[8];
+        blk[0] = arm ? (pass ? T(1) : T(0)) : qc;
+#pragma unroll
+        for (int k = 0; k < kArmDof; ++k) blk[1 + k] = qa[k];
+        blk[7] = x;
+        store_block8(ro->rec + (int64_t)(it - k0) * ro->rl + (arm ? kRecPass : kRecRoot), blk);
+      }
+      if (ended) break;
+    } else {
+      if (it >= prm.max_iters) break;  // loop exhausted: the reference never tests this iterate
+      if (both_below(x, xo, prm.eps2)) {  // |e_L| < eps and |e_R| < eps (:70)
+        conv = true;
+        break;
+      }
     }
     T q_old[7];
     q_old[0] = qc;
@@ -135,6 +201,9 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   for (int i = 0; i < 8; ++i) ps += pad[i];
   if (any_of(ps == T(-12345.678))) it = -1;  // never true; keeps the padding live
 #endif
+  if constexpr (REC) {
+    if (k0 >= 0 && arm == 0) *ro->nrec = (it - k0 + 1) | kTrajEnded;
+  }
   it_out = it;
   nrm_out = sqrt(x);
   other_out = sqrt(xo);
@@ -145,12 +214,13 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 // model-specialised kernels ikg_jit.cpp compiles at run time with `m` pointing
 // at a constant copy of the model tables): one 64-lane wave per workgroup
 // holding `ppw` problems on lanes [0, 2 ppw).
-template <typename T, bool DAMPED, class SP, bool MED>
+template <typename T, bool DAMPED, class SP, bool MED, bool REC = false>
 __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KParams<T>& prm,
                                        const T* __restrict__ targets, const T* __restrict__ q0, int64_t q0_stride,
                                        int64_t B, int64_t S, int ppw, T* __restrict__ q_out,
                                        uint8_t* __restrict__ conv_out, int32_t* __restrict__ iters_out,
-                                       T* __restrict__ err_out) {
+                                       T* __restrict__ err_out, T* __restrict__ rec = nullptr,
+                                       int32_t* __restrict__ nrec = nullptr) {
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
   const int arm = lane & 1;
@@ -166,7 +236,16 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
   int it;
   bool conv;
   T nrm, other;
-  solve_pair<T, DAMPED, SP, MED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
+  if constexpr (REC) {  // the continuation's records (ikg_collision.hip): outputs at the first passing iterate
+    const int rl = rec_len(m->n_passive);
+    const RecOut<T> ro{rec + p * (int64_t)(prm.max_iters + 1) * rl, nrec + p, qrow, q_out + p * m->nq,
+                       conv_out + p, iters_out + p, err_out + p * 2, rl};
+    if (arm == 0) nrec[p] = 0;
+    solve_pair<T, DAMPED, SP, MED, true>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro);
+    if (conv) return;
+  } else {
+    solve_pair<T, DAMPED, SP, MED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
+  }
   store_q(m, arm, qrow, it, qc, qa, q_out + p * m->nq);
   if (arm == 0) {
     if (conv_out) conv_out[p] = conv ? 1 : 0;

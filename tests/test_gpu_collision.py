@@ -204,12 +204,37 @@ def test_trajectory_continuation_equals_interleaved(csolver, dtype, monkeypatch)
 
 
 def test_trajectory_continuation_windows(csolver, solve_cases, monkeypatch):
-    """Windows shorter than the loop (several update/scan rounds, certificates
-    carried across them) give the single-window answer: IKG_TRAJ_WINDOW forces
-    16-iterate windows."""
+    """The records the pair kernel writes itself (IKG_TRAJ_REC=1, broadcast
+    q0), the trajectory kernel's (default), and the latter in 16-iterate
+    windows (several update/scan rounds, witnesses carried across them) give
+    one answer."""
     c = solve_cases
-    a = csolver.solve(c["targets"], c["q0"], check_collision=True)
+    q0 = np.zeros(15)
+    monkeypatch.setenv("IKG_TRAJ_REC", "1")
+    a = csolver.solve(c["targets"], q0, check_collision=True)
+    monkeypatch.setenv("IKG_TRAJ_REC", "0")
+    b = csolver.solve(c["targets"], q0, check_collision=True)
     monkeypatch.setenv("IKG_TRAJ_WINDOW", "16")
-    b = csolver.solve(c["targets"], c["q0"], check_collision=True)
-    assert np.array_equal(a.converged, b.converged) and np.array_equal(a.iters, b.iters)
-    assert np.abs(a.q - b.q).max() <= 1e-12
+    d = csolver.solve(c["targets"], q0, check_collision=True)
+    for x in (b, d):
+        assert np.array_equal(a.converged, x.converged) and np.array_equal(a.iters, x.iters)
+        assert np.abs(a.q - x.q).max() <= 1e-9 and np.abs(a.err - x.err).max() <= 1e-12
+    assert np.abs(b.q - d.q).max() <= 1e-12
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_records_in_batch_kernel_equal_trajectory_kernel(csolver, dtype, monkeypatch):
+    """C2's 4,096 targets from q = 0: the batch kernel's own records (it keeps
+    iterating past the first passing iterate) and the trajectory kernel's
+    recomputed ones give the same flags and update counts."""
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(4096, seed=0)
+    monkeypatch.setenv("IKG_TRAJ_REC", "1")
+    a = csolver.solve(tg, np.zeros(15), dtype=dtype, check_collision=True)
+    monkeypatch.setenv("IKG_TRAJ_REC", "0")
+    b = csolver.solve(tg, np.zeros(15), dtype=dtype, check_collision=True)
+    same = (a.converged == b.converged) & (a.iters == b.iters)
+    if dtype == "f64":
+        assert same.all() and np.abs(a.q - b.q).max() <= 1e-9
+    else:
+        assert same.mean() >= 0.99

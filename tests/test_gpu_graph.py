@@ -18,6 +18,7 @@ def _same(a, b):
     return all(bool(torch_equal(x, y)) for x, y in zip(a, b))
 
 
+
 def torch_equal(x, y):
     import torch
     return torch.equal(x, y)
@@ -54,7 +55,7 @@ def test_batch_solve_replays_from_a_graph(collision):
         x.zero_()
     g.replay()
     torch.cuda.synchronize()
-    assert _same(out, ref)
+    assert _same(out, ref), _diff(out, ref)
     # replays read the inputs in place: new targets, new answers
     tg.copy_(torch.tensor(uniform_targets(1024, seed=4), dtype=torch.float64, device=dev))
     g.replay()
@@ -62,7 +63,7 @@ def test_batch_solve_replays_from_a_graph(collision):
     ref2 = _bufs(torch, 1024, torch.float64, dev)
     s.solve_into(tg, q0, *ref2, _lib.IKG_F64, torch.cuda.current_stream().cuda_stream, check_collision=collision)
     torch.cuda.synchronize()
-    assert _same(out, ref2)
+    assert _same(out, ref2), _diff(out, ref2)
     s.close()
 
 
