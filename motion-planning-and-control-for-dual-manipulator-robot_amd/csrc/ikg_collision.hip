@@ -1485,13 +1485,16 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
   const int64_t par = (int64_t)(round & 1) * w.slots;
   rec_slots(m, lane, SL);
   for (int i = blk; i < n; i += nb) {
-    if (w.done[i]) continue;  // wave-uniform
+    // answered by an earlier scan: window r - 1's, or (no pre-screen: witness0
+    // null) the first checks' before window 0
+    if ((round > 0 || (round == 0 && !witness0)) && w.done[i]) continue;  // wave-uniform
     const int64_t p = clist[i];
     const int64_t t_idx = S_per_target > 1 ? p / S_per_target : p;
     if (lane < 12) tgt[lane] = targets[t_idx * 12 + lane];
     if (lane < nq) S.par[lane] = m->jparent[lane];
     if (lane == 0) {  // the pre-screen's colliding pair, else the one the last window ended with
-      W.pair = round < 0 ? -1 : (witness0 && round == 0) ? witness0[p] : w.cst[i].pair;
+      const int wp0 = round < 0 ? -1 : (witness0 && round == 0) ? witness0[p] : w.cst[i].pair;
+      W.pair = wp0 >= 0 && wp0 < c->n_pairs ? wp0 : -1;  // a witness is only a hint: never trust an index
       W.cert_ok = 0;
     }
     if (round < 0 && lane < nq) S.q[lane] = q_out[p * nq + lane];
