@@ -56,6 +56,8 @@ struct ikg_model {
   // dtype (0 = f64, 1 = f32), loaded modules per device
   std::vector<char> jit_code[2];
   std::vector<ikg::JitKernels*> jit[2];
+  // scratch of solves captured into graphs (ikg_launch.hpp ws_alloc), freed here
+  ikg::WsOwner ws;
 
   template <typename T>
   const ikg::JitKernels* jit_kernels(int device) {
@@ -208,17 +210,18 @@ ikg::KParams<T> kparams(const ikg_params* p) {
   return ikg::make_kparams<T>(p);
 }
 
-// Records in the batch kernel for the collision continuation (IKG_TRAJ_REC=1;
-// by default the trajectory kernel recomputes the updates past the first
-// passing iterate).  Opt-in: like IKG_TRAJ_PRESCREEN=0, it showed graph
-// replays that differed from the direct solve in tests/test_gpu_graph.py
-// runs (not reproduced outside pytest).  Up to kRecBudget
-// bytes of records per solve.
+// Records in the batch kernel for the collision continuation (the default
+// since round 3: C2 with the collision term 1.62 -> 1.30 ms; IKG_TRAJ_REC=0
+// selects the trajectory kernel, which recomputes the updates past the first
+// passing iterate).  Its round-2 graph-replay mismatch was the graph memory
+// node the records came from (ws_alloc, ikg_launch.hpp).  Up
+// to kRecBudget bytes of records per solve.
 static bool rec_in_batch() {
   const char* e = getenv("IKG_TRAJ_REC");
-  return e && atoi(e) != 0;
+  return !(e && atoi(e) == 0);
 }
 constexpr size_t kRecBudget = size_t(1) << 30;
+
 
 template <typename T>
 int solve_batch_t(ikg_model* model, int device, const void* targets, const void* q0, int64_t q0_stride, int64_t B,
@@ -231,6 +234,7 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   if (params->check_collision && (rc = model->collision_tables<T>(device, &dc))) return rc;
   const int nq = model->desc.nq;
   ikg::BatchArgs a{targets, q0, q0_stride, B, q_out, converged, iters, err_out, 32};
+  a.ws_owner = &model->ws;
   a.ppw = params->problems_per_wave > 0 ? params->problems_per_wave : auto_ppw(device, B);
   a.variant = params->variant;
   if (params->variant == IKG_VARIANT_PACKED && (sizeof(T) != 4 || model->spec != ikg::kSpecNextage || params->lambda > 0))
@@ -266,9 +270,12 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
       rec_in_batch()) {
     const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
     const size_t b_rec = (sizeof(T) * rl * ((size_t)params->max_iters + 1) * (size_t)B + 255) & ~(size_t)255;
-    if (b_rec <= kRecBudget && hipMallocAsync(&rec, b_rec + sizeof(int32_t) * (size_t)B, s) == hipSuccess) {
+    if (b_rec <= kRecBudget && ikg::ws_alloc(&model->ws, &rec, b_rec + sizeof(int32_t) * (size_t)B, s) == hipSuccess) {
       a.rec = rec;
       a.rec_n = (int32_t*)((char*)rec + b_rec);
+      ikg::ws_trace("alloc rec", rec, b_rec + sizeof(int32_t) * (size_t)B, s);
+      ikg::poison_float(rec, b_rec, s);
+      ikg::poison_int(a.rec_n, sizeof(int32_t) * (size_t)B, s);
       a.rec_used = &rec_used;
     } else {
       rec = nullptr;
@@ -277,13 +284,17 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   }
   hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, model->spec, s);
   if (e != hipSuccess) {
-    if (rec) (void)hipFreeAsync(rec, s);
+    if (rec) {
+      ikg::ws_trace("free rec", rec, 0, s);
+      (void)ikg::ws_free(&model->ws, rec, s);
+    }
     return hip_fail(e, "ikg pair kernel launch");
   }
   if (dc) {
     e = ikg::launch_collide_continue<T>(dm, dc, kparams<T>(params), a, model->spec, nq, model->c64.n_geoms, s);
     if (rec) {
-      const hipError_t ef = hipFreeAsync(rec, s);
+      ikg::ws_trace("free rec", rec, 0, s);
+      const hipError_t ef = ikg::ws_free(&model->ws, rec, s);
       if (e == hipSuccess) e = ef;
     }
     if (e != hipSuccess) return hip_fail(e, "ikg collision continuation launch");
@@ -312,6 +323,7 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
                    nullptr, nullptr, nullptr, nullptr};
   a.variant = params->variant;
   a.jit = model->jit_kernels<T>(device);
+  a.ws_owner = &model->ws;
   if (params->variant == IKG_VARIANT_PACKED && (sizeof(T) != 4 || model->spec != ikg::kSpecNextage || params->lambda > 0))
     return fail(IKG_EINVAL, "variant PACKED needs fp32, a Nextage-class model and lambda = 0");
   if (params->variant == IKG_VARIANT_QUAD && (model->spec != ikg::kSpecNextage || params->lambda > 0))
@@ -338,16 +350,20 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   const int64_t n = T_ * S;
   const size_t b_q = sizeof(T) * nq * n, b_err = sizeof(T) * 2 * n, b_it = sizeof(int32_t) * n;
   char* ws = nullptr;
-  hipError_t e = hipMallocAsync((void**)&ws, b_q + b_err + b_it + n + 64, s);
-  if (e != hipSuccess) return fail(IKG_ENOMEM, "hipMallocAsync(multistart workspace): %s", hipGetErrorString(e));
+  hipError_t e = ikg::ws_alloc(&model->ws, (void**)&ws, b_q + b_err + b_it + n + 64, s);
+  if (e != hipSuccess) return fail(IKG_ENOMEM, "multistart workspace allocation: %s", hipGetErrorString(e));
+  ikg::ws_trace("alloc multistart", ws, b_q + b_err + b_it + n + 64, s);
+  ikg::poison_float(ws, b_q + b_err, s);
+  ikg::poison_int(ws + b_q + b_err, b_it + n, s);
   a.ws_q = ws;
   a.ws_err = ws + b_q;
   a.ws_iters = (int32_t*)(ws + b_q + b_err);
   a.ws_conv = (uint8_t*)(ws + b_q + b_err + b_it);
   e = ikg::launch_multistart<T>(dm, kparams<T>(params), a, model->spec, s);
-  hipError_t e2 = hipFreeAsync(ws, s);
+  ikg::ws_trace("free multistart", ws, 0, s);
+  hipError_t e2 = ikg::ws_free(&model->ws, ws, s);
   if (e != hipSuccess) return hip_fail(e, "ikg multistart kernel launch");
-  if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync(multistart workspace)");
+  if (e2 != hipSuccess) return hip_fail(e2, "multistart workspace free");
   if (host) {
     st.back(q_out, a.q_out, sizeof(T) * nq * T_);
     st.back(converged, a.converged, T_);
@@ -554,6 +570,12 @@ void ikg_model_destroy(ikg_model* m) {
         ikg::jit_unload(*v[i]);
         delete v[i];
       }
+  // scratch held by captured graphs (the graphs must be gone by now: they
+  // also reference the model tables freed above)
+  for (auto& b : m->ws.bufs) {
+    (void)hipSetDevice(b.first);
+    (void)hipFree(b.second);
+  }
   if (prev >= 0) (void)hipSetDevice(prev);
   delete m;
 }

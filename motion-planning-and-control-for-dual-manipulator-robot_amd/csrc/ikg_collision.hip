@@ -1339,9 +1339,15 @@ __device__ __forceinline__ void traj_window(const KModel<T>* __restrict__ m, con
   for (int base = blk * ppw; base < n; base += nb * ppw) {
     const int i = base + (lane >> 1);
     if (lane >= 2 * ppw || i >= n) continue;  // both lanes of a pair together
-    // answered, or its loop already exhausted (the scan of that window, running
-    // beside this one, answers it); `done` may be stale here: extra work only
-    if (round > 0 && (w.done[i] || w.itrun[i] >= prm.max_iters)) continue;
+    // answered, or its loop already exhausted: the window before recorded the
+    // iterate after max_iters (itrun = max_iters + 1 marks that), and its scan,
+    // running beside this window, answers it.  `done` may be stale here: extra
+    // work only.  A skipped problem's record count is cleared, so the scan of
+    // this window never reads the slot's records from two windows back.
+    if (round > 0 && (w.done[i] || w.itrun[i] > prm.max_iters)) {
+      if (arm == 0) w.nrec[par + i] = 0;
+      continue;
+    }
     const int64_t p = clist[i];
     const int64_t tgt = S_per_target > 1 ? p / S_per_target : p;
     T RT[9], tT[3], qc, qa[kArmDof], sn[7], cs[7];
@@ -1407,7 +1413,9 @@ __device__ __forceinline__ void traj_window(const KModel<T>* __restrict__ m, con
       for (int k = 0; k < kArmDof; ++k) qr[arm ? m->arm_q[1][k] : m->arm_q[0][k]] = qa[k];
     }
     if (arm == 0) {
-      w.itrun[i] = it;
+      // a window that stops at it == max_iters without having recorded that
+      // iterate (it0 + Wn == max_iters) is not `ended`: the next one records it
+      w.itrun[i] = ended ? prm.max_iters + 1 : it;
       w.nrec[par + i] = j | (ended ? kTrajEnded : 0);
     }
   }
@@ -1762,9 +1770,13 @@ static bool traj_fuse() {
   return !(e && atoi(e) == 0);
 }
 
-// record window per problem: the whole remainder of the loop (max_iters + 1
-// records) when the record buffer stays under kTrajBudget, else windows of
-// at least 16 iterates, one (update, scan) round each
+// record window per problem: kTrajWindow iterates per (update, scan) round,
+// fewer (at least 16) when two buffers of Wn records for every problem of the
+// launch would exceed kTrajBudget.  The buffers are sized by the whole batch B
+// because the number of problems that continue is only known on the device:
+// 2 x 128 x rec_len x sizeof(T) = 40 KB per problem in fp64 (164 MB at C2,
+// 2.7 GB at B = 65,536).  Windows are relative to each problem's first
+// passing iterate; every problem needs ceil((max_iters + 1 - k0) / Wn) rounds.
 constexpr size_t kTrajBudget = size_t(4) << 30;
 constexpr int kTrajWindow = 128;
 
@@ -1788,7 +1800,7 @@ static hipError_t launch_traj_t(const KModel<T>* dm, const KCollision<T>* dc, co
   const size_t b_rec = al(per * Wn), b_q = al(sizeof(T) * nq * B), b_i = al(sizeof(int32_t) * B),
                b_c = al(sizeof(TrajCert<T>) * B);
   char* ws = nullptr;
-  hipError_t e = hipMallocAsync((void**)&ws, b_rec + b_q + 6 * b_i + b_c, s);
+  hipError_t e = ws_alloc(a.ws_owner, (void**)&ws, b_rec + b_q + 6 * b_i + b_c, s);
   if (e != hipSuccess) return e;
   TrajWs<T> w;
   char* c = ws;
@@ -1800,6 +1812,9 @@ static hipError_t launch_traj_t(const KModel<T>* dm, const KCollision<T>* dc, co
   w.done = (int32_t*)c, c += b_i;
   w.cst = (TrajCert<T>*)c;
   w.slots = (int64_t)B;
+  ws_trace("alloc traj", ws, b_rec + b_q + 6 * b_i + b_c, s);
+  poison_float(w.rec, b_rec + b_q, s);  // records, qrun
+  poison_int(w.itrun, 6 * b_i + b_c, s);  // itrun, it0, nrec, done, cst
   hipLaunchKernelGGL(ikg_fill_i32_kernel, dim3((unsigned)((B + 255) / 256)), dim3(256), 0, s, w.done, a.B, 0);
   const int32_t* wit0 = first ? nullptr : (const int32_t*)cw.wit;
   const int32_t* clist = (const int32_t*)cw.clist;
@@ -1824,7 +1839,8 @@ static hipError_t launch_traj_t(const KModel<T>* dm, const KCollision<T>* dc, co
                        (T*)a.q_out, a.converged, a.iters, (T*)a.err_out);
   }
   e = hipGetLastError();
-  const hipError_t ef = hipFreeAsync(ws, s);
+  ws_trace("free traj", ws, 0, s);
+  const hipError_t ef = ws_free(a.ws_owner, ws, s);
   return e != hipSuccess ? e : ef;
 }
 
@@ -1869,10 +1885,13 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
   // stream-ordered workspace: the pre-screen's witness pair per problem
   const size_t ib = ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255);
   char* ws = nullptr;
-  hipError_t e = hipMallocAsync((void**)&ws, 3 * ib + 256 + sizeof(T) * kStretchRec * (size_t)a.B, s);
+  hipError_t e = ws_alloc(a.ws_owner, (void**)&ws, 3 * ib + 256 + sizeof(T) * kStretchRec * (size_t)a.B, s);
   if (e != hipSuccess) return e;
   ContWs<T> w{(int32_t*)ws, (int32_t*)(ws + ib), (int32_t*)(ws + 3 * ib), (int32_t*)(ws + 2 * ib),
               (T*)(ws + 3 * ib + 256)};
+  ws_trace("alloc cont", ws, 3 * ib + 256 + sizeof(T) * kStretchRec * (size_t)a.B, s);
+  poison_int(ws, 3 * ib + 256, s);  // witness, lists, counts
+  poison_float(w.rec, sizeof(T) * kStretchRec * (size_t)a.B, s);
   // trajectory continuation without a pre-screen: the first checks run in its
   // first launch, so every converged problem is listed
   const bool first = !(a.rec_used && *a.rec_used) && cont_traj(a.B) && !traj_prescreen(a.B);
@@ -1892,7 +1911,7 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
   hipError_t ec = hipSuccess;
   if (a.rec_used && *a.rec_used) {  // the pair kernel recorded every iterate from the first passing one
     char* dws = nullptr;
-    e = hipMallocAsync((void**)&dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
+    e = ws_alloc(a.ws_owner, (void**)&dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     if (e != hipSuccess) return e;
     TrajWs<T> tw{};
     tw.rec = (T*)a.rec;
@@ -1902,13 +1921,16 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     tw.cst = (TrajCert<T>*)(dws + ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255));
     tw.slots = a.B;
     tw.by_p = 1;
+    ws_trace("alloc scan", dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
+    poison_int(dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     hipLaunchKernelGGL(ikg_fill_i32_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s, tw.done, a.B, 0);
     hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)std::min<int64_t>(1024, a.B)), dim3(64), 0, s, dm, dc,
                        (const T*)a.targets, a.S, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
                        (const int32_t*)w.wit, tw, prm.max_iters + 1, 0, (T*)a.q_out, a.converged, a.iters,
                        (T*)a.err_out);
     ec = hipGetLastError();
-    const hipError_t ef2 = hipFreeAsync(dws, s);
+    ws_trace("free scan", dws, 0, s);
+    const hipError_t ef2 = ws_free(a.ws_owner, dws, s);
     if (ec == hipSuccess) ec = ef2;
   } else if (spec == kSpecNextage) {
     if (damped)
@@ -1923,7 +1945,8 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     launch_continue_sel<T, false, SpecGeneric>(dm, dc, prm, a, nq, ng, w, s, ec, first);
   }
   e = ec != hipSuccess ? ec : hipGetLastError();
-  const hipError_t ef = hipFreeAsync(ws, s);
+  ws_trace("free cont", ws, 0, s);
+  const hipError_t ef = ws_free(a.ws_owner, ws, s);
   return e != hipSuccess ? e : ef;
 }
 

@@ -318,6 +318,7 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   // S == 1: the one seed row serves every target (broadcast), since the batch
   // kernel indexes q0 rows by problem when S == 1
   BatchArgs b{a.targets, a.seeds, a.S == 1 ? 0 : a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
+  b.ws_owner = a.ws_owner;
   b.jit = a.jit;
   // AUTO keeps the pair layout here: seeds spread the update counts, and a
   // wave lasts as long as its slowest problem -- 64 per packed wave against 32

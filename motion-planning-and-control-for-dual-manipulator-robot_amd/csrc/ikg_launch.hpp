@@ -3,6 +3,12 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <mutex>
+#include <utility>
+#include <vector>
 
 #include "ikg_collision.hpp"
 #include "ikg_device.hpp"
@@ -10,6 +16,50 @@
 namespace ikg {
 
 struct JitKernels;  // ikg_jit.hpp
+
+// Workspaces of captured solves.  Outside a stream capture a
+// solve's scratch is stream-ordered: hipMallocAsync / hipFreeAsync.  Inside a
+// capture those calls become graph memory nodes, and a 164 MB record buffer
+// taken that way read back as zeros in a later replay after a process had
+// used the default pool heavily (tests/test_gpu_graph.py with
+// IKG_TRAJ_REC=1; the same buffer from hipMalloc passed every replay).  So a
+// captured solve takes its scratch from hipMalloc (relaxed capture mode for
+// the call), owned by the model until ikg_model_destroy: a graph replays
+// with memory nobody else maps, and a graph never runs two replays at once.
+struct WsOwner {
+  std::mutex mu;
+  std::vector<std::pair<int, void*>> bufs;  // (device, pointer)
+};
+
+inline bool stream_capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+}
+
+inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s) {
+  *p = nullptr;
+  if (!owner || !stream_capturing(s)) return hipMallocAsync(p, bytes, s);
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  const hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return e;
+  }
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lock(owner->mu);
+  owner->bufs.emplace_back(dev, *p);
+  return hipSuccess;
+}
+
+// the matching free: a captured solve's buffer stays with the owner
+inline hipError_t ws_free(WsOwner* owner, void* p, hipStream_t s) {
+  if (!p) return hipSuccess;
+  if (owner && stream_capturing(s)) return hipSuccess;
+  return hipFreeAsync(p, s);
+}
 
 struct BatchArgs {
   const void* targets;
@@ -31,6 +81,7 @@ struct BatchArgs {
   void* rec = nullptr;
   int32_t* rec_n = nullptr;
   bool* rec_used = nullptr;
+  WsOwner* ws_owner = nullptr;  // scratch of captured solves (ws_alloc)
 };
 
 struct MultiArgs {
@@ -55,7 +106,37 @@ struct MultiArgs {
   int n_geoms = 0;
   int variant = 0;  // ikg_variant of the per-seed solves
   const JitKernels* jit = nullptr;
+  WsOwner* ws_owner = nullptr;
 };
+
+// Debug knob IKG_POISON=1 (read per call): every stream-ordered workspace is
+// filled right after its allocation, so a read of memory the solve did not
+// write gives a wrong answer on the first run instead of stale data from an
+// earlier solve or graph replay.  Integer arrays (counts, indices, flags) get
+// 0xFF bytes (-1: "nothing recorded", never an index that is used); floating
+// arrays get 0x7F bytes (1.4e306 / 3.4e38: finite, so no -ffinite-math-only
+// code sees a NaN, but absurd as a joint angle or an error norm).
+inline bool ws_poison() {
+  const char* e = getenv("IKG_POISON");
+  return e && atoi(e) != 0;
+}
+inline void poison_int(void* p, size_t bytes, hipStream_t s) {
+  if (p && bytes && ws_poison()) (void)hipMemsetAsync(p, 0xFF, bytes, s);
+}
+inline void poison_float(void* p, size_t bytes, hipStream_t s) {
+  if (p && bytes && ws_poison()) (void)hipMemsetAsync(p, 0x7F, bytes, s);
+}
+
+// Debug knob IKG_WS_TRACE=1: every stream-ordered workspace allocation and
+// free is printed (address range, whether the stream is capturing).
+inline void ws_trace(const char* what, const void* p, size_t bytes, hipStream_t s) {
+  const char* e = getenv("IKG_WS_TRACE");
+  if (!(e && atoi(e) != 0)) return;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(s, &st);
+  fprintf(stderr, "[ikg ws] %s %p +%zu -> %p%s\n", what, p, bytes, (const void*)((const char*)p + bytes),
+          st == hipStreamCaptureStatusActive ? " (capturing)" : "");
+}
 
 // kernel specialisation chosen at model creation (ikg_model_build.hpp)
 constexpr int kSpecGeneric = 0;

@@ -19,16 +19,22 @@ from __future__ import annotations
 import numpy as np
 
 from .config import CUBE_PLACEMENT, CUBE_PLACEMENT_TARGET, EPSILON, DT_IK, MAX_ITERS  # noqa: F401
+from .pinocchio_bridge import is_pinocchio_like, solver_for
 from .se3 import as_rt, pack_targets
 from .tools import setcubeplacement
 
 
-def _solver_of(robot):
+def _solver_of(robot, cube=None):
+    """ikgrasp's own Robot carries its solver; a Pinocchio RobotWrapper (or
+    any object with its attribute surface) gets one built from its model,
+    the cube's hook frames and its collision model (pinocchio_bridge)."""
     solver = getattr(robot, "solver", None)
-    if solver is None:
-        raise TypeError(f"robot of type {type(robot).__name__} carries no ikgrasp solver; "
-                        "build it with ikgrasp.scene.setuppinocchio()")
-    return solver
+    if solver is not None:
+        return solver
+    if is_pinocchio_like(robot):
+        return solver_for(robot, cube, device=getattr(robot, "device", 0))
+    raise TypeError(f"robot of type {type(robot).__name__} carries no ikgrasp solver and no Pinocchio-style "
+                    "model; build it with ikgrasp.scene.setuppinocchio()")
 
 
 def computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None):
@@ -37,7 +43,7 @@ def computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None):
     R, t = as_rt(cubetarget)
     target = np.concatenate([R.reshape(9), t])[None, :]
     q0 = np.array(qcurrent, dtype=np.float64).copy()  # :49
-    solver = _solver_of(robot)
+    solver = _solver_of(robot, cube)
     sol = solver.solve(target, q0, dtype="f64", eps=EPSILON, dt=DT_IK, max_iters=MAX_ITERS,
                        check_collision=solver.scene is not None)
     q = sol.q[0].astype(np.float64)
@@ -46,23 +52,23 @@ def computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None):
     return q, bool(sol.converged[0])
 
 
-def computeqgrasppose_batch(robot, qcurrent, cubetargets, dtype="f64", **kw):
+def computeqgrasppose_batch(robot, qcurrent, cubetargets, dtype="f64", cube=None, **kw):
     """Batched API: cubetargets [B,12] / [B,4,4] / list of SE3; qcurrent [nq]
     (broadcast) or [B,nq] -> (q [B,nq], success [B], iters [B]).  `success`
     includes the collision term when the robot has a scene (override with
-    check_collision=False)."""
+    check_collision=False).  `cube`: needed once for a Pinocchio-style robot."""
     targets = pack_targets(cubetargets)
-    solver = _solver_of(robot)
+    solver = _solver_of(robot, cube)
     kw.setdefault("check_collision", solver.scene is not None)
     sol = solver.solve(targets, np.asarray(qcurrent), dtype=dtype, **kw)
     return sol.q, sol.converged, sol.iters
 
 
-def computeqgrasppose_multistart(robot, seeds, cubetargets, dtype="f64", **kw):
+def computeqgrasppose_multistart(robot, seeds, cubetargets, dtype="f64", cube=None, **kw):
     """Multi-start API: seeds [S,nq] x targets -> best seed per target:
     (q [T,nq], success [T], best_seed [T])."""
     targets = pack_targets(cubetargets)
-    solver = _solver_of(robot)
+    solver = _solver_of(robot, cube)
     kw.setdefault("check_collision", solver.scene is not None)
     sol = solver.solve_multistart(targets, np.asarray(seeds), dtype=dtype, **kw)
     return sol.q, sol.converged, sol.best_seed

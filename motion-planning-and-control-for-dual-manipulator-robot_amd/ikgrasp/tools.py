@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import numpy as np
 
+from .pinocchio_bridge import is_pinocchio_like, solver_for, target_placement
 from .se3 import SE3, as_rt
 
 
@@ -41,7 +42,16 @@ def getcubeplacement(cube, hookname=None):
 
 def setcubeplacement(robot, cube, oMf):
     """tools.py:62-68 — place the cube (and the robot's copy of its collision
-    geometry) at oMf.  Callers rely on this side effect (path.py:61)."""
+    geometry) at oMf.  Callers rely on this side effect (path.py:61).  A
+    Pinocchio RobotWrapper gets the reference's assignments (the last robot
+    geometry, the cube's geometry; the cube's updateGeometryPlacements, a
+    Pinocchio call, is not repeated)."""
+    if not hasattr(robot, "solver") and is_pinocchio_like(robot):
+        for model, idx in ((getattr(robot, "visual_model", None), -1), (getattr(robot, "collision_model", None), -1),
+                           (getattr(cube, "visual_model", None), -1), (getattr(cube, "collision_model", None), 0)):
+            if model is not None:
+                model.geometryObjects[idx].placement = oMf
+        return
     R, t = as_rt(oMf)
     cube.placement = SE3(R, t)
     robot.cube_placement = cube.placement
@@ -50,23 +60,21 @@ def setcubeplacement(robot, cube, oMf):
 def collision(robot, q):
     """tools.py:25-35 — True if any active pair of the scene intersects at q
     (the cube geometry sits where setcubeplacement last put it)."""
-    solver = robot.solver
-    if solver.scene is None:
-        raise RuntimeError("robot has no collision scene attached (ikgrasp.scene.setuppinocchio builds it)")
-    placement = robot.cube_placement if robot.cube_placement is not None else robot.cube_default
-    R, t = as_rt(placement)
-    target = np.concatenate([R.reshape(9), t])[None, :]
+    solver, _ = _scene_of(robot)
+    target = _cube_target(robot)
     return bool(solver.collision(np.asarray(q, dtype=np.float64).reshape(1, -1), target)[0])
 
 
 def _scene_of(robot):
-    solver = robot.solver
+    solver = robot.solver if hasattr(robot, "solver") or not is_pinocchio_like(robot) else solver_for(robot)
     if solver.scene is None:
         raise RuntimeError("robot has no collision scene attached (ikgrasp.scene.setuppinocchio builds it)")
     return solver, solver.scene
 
 
 def _cube_target(robot):
+    if not hasattr(robot, "solver") and is_pinocchio_like(robot):
+        return target_placement(robot)
     placement = robot.cube_placement if robot.cube_placement is not None else robot.cube_default
     R, t = as_rt(placement)
     return np.concatenate([R.reshape(9), t])[None, :]

@@ -123,7 +123,7 @@ def test_dropin_uses_collision_and_reproduces_kats(kat):
     assert not collision(robot, qe)
 
 
-def test_multistart_with_collision_matches_single_solves(csolver, solve_cases):
+def test_multistart_with_collision_matches_single_solves(csolver, solve_cases, monkeypatch):
     c = solve_cases
     tg = c["targets"][:16]
     seeds = np.stack([np.zeros(15)] + [c["q0"][-k] for k in range(1, 4)])
@@ -133,7 +133,15 @@ def test_multistart_with_collision_matches_single_solves(csolver, solve_cases):
         b = ms.best_seed[t]
         assert ms.converged[t] == per[b].converged[t]
         assert ms.converged[t] == any(p.converged[t] for p in per)
-        assert np.array_equal(ms.q[t], per[b].q[t])
+        assert ms.iters[t] == per[b].iters[t]
+        # a broadcast seed's records come from the batch kernel (trig state
+        # carried on), per-problem seeds' from the trajectory kernel (trig
+        # resynced at each window): the same iterates to rounding
+        assert np.abs(ms.q[t] - per[b].q[t]).max() <= 1e-9
+    monkeypatch.setenv("IKG_TRAJ_REC", "0")
+    per0 = [csolver.solve(tg, s, check_collision=True) for s in seeds]
+    for t in range(len(tg)):
+        assert np.array_equal(ms.q[t], per0[ms.best_seed[t]].q[t])  # same schedule: bit for bit
 
 
 def test_check_collision_without_scene_fails_loudly(solver):
@@ -238,3 +246,55 @@ def test_records_in_batch_kernel_equal_trajectory_kernel(csolver, dtype, monkeyp
         assert same.all() and np.abs(a.q - b.q).max() <= 1e-9
     else:
         assert same.mean() >= 0.99
+
+
+@pytest.mark.parametrize("poison", ["0", "1"])
+def test_trajectory_window_ending_at_max_iters(csolver, solve_cases, oracle_cases, monkeypatch, poison):
+    """A record window that stops exactly at update max_iters without having
+    recorded that iterate (k0 + m * Wn == max_iters) must hand it to the next
+    window: the reference returns success = False at the iterate after
+    max_iters updates (inverse_geometry.py:56, :97-98).  Every run-on fixture
+    problem is solved alone with Wn = (1000 - k0) / m for m = 1, 2 where that
+    is a whole window of >= 16; with IKG_POISON=1 every workspace starts as
+    garbage, so a read of a slot this solve did not write shows up."""
+    c = solve_cases
+    monkeypatch.setenv("IKG_POISON", poison)
+    cont = np.nonzero(oracle_cases["converged"] & ~c["success"])[0]
+    assert len(cont) >= 5
+    ran = 0
+    for i in cont:
+        k0 = int(oracle_cases["iters"][i])
+        for mwin in (1, 2):
+            if (1000 - k0) % mwin or (1000 - k0) // mwin < 16:
+                continue
+            monkeypatch.setenv("IKG_TRAJ_WINDOW", str((1000 - k0) // mwin))
+            sol = csolver.solve(c["targets"][i:i + 1], c["q0"][i:i + 1], check_collision=True)
+            assert not sol.converged[0] and sol.iters[0] == 1000, (i, k0, mwin)
+            assert np.abs(sol.err[0] - c["err"][i]).max() <= 1e-9
+            assert csolver.collision(sol.q, c["targets"][i:i + 1]).all()
+            ran += 1
+    assert ran >= 5
+
+
+def test_poisoned_workspaces_give_the_same_answers(csolver, solve_cases, monkeypatch):
+    """IKG_POISON=1 fills every stream-ordered workspace with garbage before
+    use: each schedule of the continuation must still give the fixture answers
+    (nothing is read before this solve writes it)."""
+    c = solve_cases
+    monkeypatch.setenv("IKG_POISON", "1")
+    base = csolver.solve(c["targets"], c["q0"], check_collision=True)
+    assert np.array_equal(base.converged, c["success"]) and np.array_equal(base.iters, c["iters"])
+    for env in ({"IKG_TRAJ_REC": "1"}, {"IKG_TRAJ_PRESCREEN": "0"}, {"IKG_TRAJ_WINDOW": "16"},
+                {"IKG_CONT_TRAJ": "0"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        sol = csolver.solve(c["targets"], c["q0"], check_collision=True)
+        ref = base
+        if "IKG_TRAJ_REC" in env:  # the batch kernel records for a broadcast q0 only
+            sol = csolver.solve(c["targets"], np.zeros(15), check_collision=True)
+            monkeypatch.setenv("IKG_TRAJ_REC", "0")
+            ref = csolver.solve(c["targets"], np.zeros(15), check_collision=True)
+        assert np.all(np.isfinite(sol.q)) and np.abs(sol.q).max() < 10, env
+        assert np.array_equal(sol.converged, ref.converged) and np.array_equal(sol.iters, ref.iters), env
+        for k in env:
+            monkeypatch.delenv(k)
