@@ -682,10 +682,7 @@ __device__ __forceinline__ T cont_step(const KModel<T>* __restrict__ m, const KP
     x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
   T alpha, beta;
   if constexpr (!DAMPED) {
-    T u[6], v[6];
-    arm_solve<T, SP>(st, u, v, alpha, beta);
-    s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
-    arm_dq(u, v, s, dq);
+    pinv_step_cf<T, SP>(st, arm, m->sing_tau, dq, s);
   } else {
     T A[6][8], ze[6], zc[6];
     arm_system(st, A);
@@ -738,10 +735,7 @@ __device__ __forceinline__ T stretch_step(const KModel<T>* __restrict__ m, const
     ArmStateF1<T> st;
     const T x = arm_fk_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, (IKG_THETA_TRACK && is_f64<T>) ? tk : nullptr,
                                        resync);
-    T u[6], v[6], alpha, beta;
-    arm_solve_f1<T, SP>(m, arm, st, sn, cs, u, v, alpha, beta);
-    s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
-    arm_dq(u, v, s, dq);
+    pinv_step_f1<T, SP>(m, arm, st, sn, cs, dq, s);
     return x;
   } else {
     return cont_step<T, DAMPED, SP, false>(m, prm, arm, sn, cs, RT, tT, nullptr, dq, s, tk, resync);
@@ -832,8 +826,16 @@ __device__ __noinline__ void cert_stretch(const KModel<T>* __restrict__ m, int m
   for (int k = 0; k < kArmDof; ++k) qa_io[k] = qa[k];
 }
 
+// occupancy the guarded step's cold LQ branch (pinv_step_*) must not cost:
+// the register bound of the kernels before it (spills go to that branch)
+template <typename T, bool DAMPED, class SP>
+constexpr int kContMinWaves = (sizeof(T) == 4 && kFrame1<SP> && !DAMPED) ? 2 : 1;
+template <typename T, bool DAMPED, class SP>
+constexpr int kStretchMinWaves = (kFrame1<SP> && !DAMPED) ? (sizeof(T) == 8 ? 2 : 4) : 1;
+
 template <typename T, bool DAMPED, class SP, int G>
-__global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T>* __restrict__ m,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kContMinWaves<T, DAMPED, SP>)))
+void ikg_collide_continue_kernel(const KModel<T>* __restrict__ m,
                                                                   const KCollision<T>* __restrict__ c,
                                                                   KParams<T> prm, const T* __restrict__ targets,
                                                                   int64_t S_per_target, int64_t B,
@@ -1106,7 +1108,8 @@ __global__ __launch_bounds__(64) void ikg_collide_continue_kernel(const KModel<T
 // pass once the margin is spent (witness[p] back to the pair: the next
 // continuation launch redoes that iterate with a real check).
 template <typename T, bool DAMPED, class SP>
-__global__ __launch_bounds__(64) void ikg_cert_stretch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? kStretchMinWaves<T, DAMPED, SP> : 1)))
+void ikg_cert_stretch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                                                               const T* __restrict__ targets, int64_t S_per_target,
                                                               T* __restrict__ q_out, uint8_t* __restrict__ conv,
                                                               int32_t* __restrict__ iters, T* __restrict__ err,
@@ -1615,7 +1618,8 @@ __device__ __noinline__ void traj_scan(const KModel<T>* __restrict__ m, const KC
 
 // Separate launches (IKG_TRAJ_FUSE=0): window r's updates, then its scan.
 template <typename T, bool DAMPED, class SP>
-__global__ __launch_bounds__(64) void ikg_traj_update_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kStretchMinWaves<T, DAMPED, SP>)))
+void ikg_traj_update_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                                                              const T* __restrict__ targets, int64_t S_per_target,
                                                              const T* __restrict__ q_out,
                                                              const int32_t* __restrict__ iters,

@@ -58,6 +58,17 @@
 #define IKG_THETA_ASIN 1
 #endif
 
+// Relative tolerance of the singularity guard (pinv_step): an arm block whose
+// closed-form inverse scale exceeds 1/tau takes the LQ form.  fp64: the
+// closed form's error grows like ~6e-19/delta at a wrist offset delta from
+// the singular angle (tools/singular_probe.py), 1e-6 keeps it below 1e-12.
+#ifndef IKG_SING_TAU64
+#define IKG_SING_TAU64 1e-6
+#endif
+#ifndef IKG_SING_TAU32
+#define IKG_SING_TAU32 1e-3
+#endif
+
 namespace ikg {
 
 constexpr int kArmDof = 6;
@@ -99,6 +110,12 @@ struct KModel {
   T jt[kMaxNq][3];
   int32_t jaxis[kMaxNq];
   int32_t jparent[kMaxNq];
+  // singularity guard of the closed-form arm solve (pinv_step, build_kmodel):
+  // relative tolerance tau of this precision, and tau * L, tau * L^2 with L the
+  // arm's shoulder-to-wrist link length sum (shoulder: |w_x|, elbow: |det2|)
+  T sing_tau;
+  T sing_wx[2];
+  T sing_det2[2];
 };
 
 // ---------------------------------------------------------------- kernel specialisation
@@ -175,6 +192,8 @@ IKG_HD inline bool all_of(bool m) { return m; }
 IKG_HD inline bool all_of(v2i m) { return m.x != 0 && m.y != 0; }
 IKG_HD inline bool mnot(bool m) { return !m; }
 IKG_HD inline v2i mnot(v2i m) { return m == 0; }
+IKG_HD inline bool mor(bool a, bool b) { return a || b; }
+IKG_HD inline v2i mor(v2i a, v2i b) { return a | b; }
 template <typename T, typename M>
 IKG_HD inline T vsel(M m, T a, T b) {
   if constexpr (LaneT<T>::packed)
@@ -1104,7 +1123,7 @@ IKG_HD inline void pose_error_aligned(const T* Rh, const T* th, const T* RT, con
 // x = A^-1 b for both.  Diagonal entries below rcond * max|R_kk| are
 // truncated to a zero inverse (the analogue of pinv's rcond).
 template <typename T>
-IKG_HD inline void qr_solve6(T (&A)[6][8], T* x0, T* x1) {
+IKG_HD inline void qr_solve6(T (&A)[6][8], T* x0, T* x1, bool* near_singular = nullptr, T tau = T(0)) {
 #pragma unroll
   for (int k = 0; k < 5; ++k) {
     T n2 = T(0);
@@ -1132,6 +1151,12 @@ IKG_HD inline void qr_solve6(T (&A)[6][8], T* x0, T* x1) {
 #pragma unroll
   for (int k = 0; k < 6; ++k) dmax = fmax(dmax, fabs(A[k][k]));
   const T cut = dmax * Prec<T>::kRcond;
+  if (near_singular) {
+    T dmin = fabs(A[0][0]);
+#pragma unroll
+    for (int k = 1; k < 6; ++k) dmin = fmin(dmin, fabs(A[k][k]));
+    *near_singular = dmin < tau * dmax;
+  }
   T rd[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) rd[k] = fabs(A[k][k]) > cut ? T(1) / A[k][k] : T(0);
@@ -1380,12 +1405,14 @@ IKG_HD inline T dot3(const T* a, const T* b) { return a[0] * b[0] + a[1] * b[1] 
 // [g1 g2 g3]^-1 applied to b0 and b1 by the adjugate (Cramer); an exactly
 // singular block gives a zero inverse (pinv truncates only below 1e-15 sigma_max).
 template <typename T>
-IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b0, const T* b1, T* x0, T* x1) {
+IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b0, const T* b1, T* x0, T* x1,
+                               T* det_out = nullptr) {
   T r1[3], r2[3], r3[3];
   cross3(g2, g3, r1);
   cross3(g3, g1, r2);
   cross3(g1, g2, r3);
   const T det = dot3(g1, r1);
+  if (det_out) *det_out = det;
   const T rdet = vsel<T>(det != T(0), frcp(det), T(0));
   x0[0] = dot3(r1, b0) * rdet;
   x0[1] = dot3(r2, b0) * rdet;
@@ -1402,7 +1429,8 @@ IKG_HD inline void inv3_apply2(const T* g1, const T* g2, const T* g3, const T* b
 // so J_a^-1 [e c] needs two 3x3 solves.  Rows are moved from the hand point h
 // to w by v_w = v_h + w_ang x (w - h) (an invertible row operation: same u, v).
 template <typename T>
-IKG_HD inline void arm_solve_wrist(const ArmState<T>& st, T* u, T* v) {
+IKG_HD inline void arm_solve_wrist(const ArmState<T>& st, T* u, T* v, typename LaneT<T>::M* near_singular = nullptr,
+                                   T tau = T(0)) {
   const T* w = st.org[5];
   const T* ev = st.e;
   const T* ew = st.e + 3;
@@ -1426,27 +1454,34 @@ IKG_HD inline void arm_solve_wrist(const ArmState<T>& st, T* u, T* v) {
     for (int i = 0; i < 3; ++i) ow[i] = w[i] - st.org[0][i];
     cross3(st.ax[0], ow, cl);
   }
-  inv3_apply2(g[0], g[1], g[2], bl, cl, u, v);
+  T dG, dH;
+  inv3_apply2(g[0], g[1], g[2], bl, cl, u, v, &dG);
   T re[3], rcv[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     re[i] = ew[i] - (u[0] * st.ax[1][i] + u[1] * st.ax[2][i] + u[2] * st.ax[3][i]);
     rcv[i] = st.ax[0][i] - (v[0] * st.ax[1][i] + v[1] * st.ax[2][i] + v[2] * st.ax[3][i]);
   }
-  inv3_apply2(st.ax[4], st.ax[5], st.ax[6], re, rcv, u + 3, v + 3);
+  inv3_apply2(st.ax[4], st.ax[5], st.ax[6], re, rcv, u + 3, v + 3, &dH);
+  if (near_singular) {  // |det| against the product of the row norms (H: unit axes)
+    const T ng = dot3(g[0], g[0]) * dot3(g[1], g[1]) * dot3(g[2], g[2]);
+    *near_singular = mor(dG * dG < tau * tau * ng, fabs(dH) < tau);
+  }
 }
 
 // lambda = 0: u = J_a^-1 e_a, v = J_a^-1 c_a; alpha = u.v, beta = v.v.
 template <typename T, class SP>
-IKG_HD inline void arm_solve(const ArmState<T>& st, T* u, T* v, T& alpha, T& beta) {
+IKG_HD inline void arm_solve(const ArmState<T>& st, T* u, T* v, T& alpha, T& beta,
+                             typename LaneT<T>::M* near_singular = nullptr, T tau = T(0)) {
   if constexpr (IKG_ABL & 4) {
     for (int k = 0; k < 6; ++k) { u[k] = st.e[k] + st.org[k][0]; v[k] = st.ax[k][1]; }
   } else if constexpr (SP::wrist) {
-    arm_solve_wrist(st, u, v);
+    arm_solve_wrist(st, u, v, near_singular, tau);
   } else {
+    static_assert(!is_packed<T>, "the generic QR solve runs in the pair layout");
     T A[6][8];
     arm_system(st, A);
-    qr_solve6(A, u, v);
+    qr_solve6(A, u, v, near_singular, tau);
   }
   alpha = T(0);
   beta = T(0);
@@ -1561,7 +1596,8 @@ IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__
 // inv3_apply2.
 template <typename T, class SP>
 IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
-                                const T* sn, const T* cs, T* u, T* v, T& alpha, T& beta) {
+                                const T* sn, const T* cs, T* u, T* v, T& alpha, T& beta,
+                                typename LaneT<T>::M* near_singular = nullptr) {
   const bool right = arm != 0;
   const T* w = st.w;
   const T* ev = st.e;
@@ -1622,7 +1658,259 @@ IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__
     alpha += u[k] * v[k];
     beta += v[k] * v[k];
   }
+  if (near_singular) {  // shoulder (w_x), elbow (det2) or wrist (c4) below the guard (pinv_step)
+    const T twx = armc<T>(right, m->sing_wx[0], m->sing_wx[1]);
+    const T tdet = armc<T>(right, m->sing_det2[0], m->sing_det2[1]);
+    *near_singular = mor(mor(fabs(w[0]) < twx, fabs(det2) < tdet), fabs(c4) < T(m->sing_tau));
+  }
 }
+
+// ---------------------------------------------------------------- singular arm blocks
+// pinv(J) e for J = [c | blockdiag(J_L, J_R)] without inverting the arm
+// blocks, for the iterates where one of them is (nearly) singular.  Per arm,
+// M_a = [c_a | J_a] (6 x 7) has full row rank even when J_a does not; with
+// z_a its minimum-norm solution of M_a z = e_a and n_a its unit null vector
+// (Householder LQ), the solutions sharing the chest value s are
+// z_a + t_a n_a, s = a_a + t_a b_a (a = z[0], b = n[0]), and
+//   min  s^2 + |x_L|^2 + |x_R|^2 = |z_L|^2 + |z_R|^2 - s^2
+// over them is attained at
+//   s = (a_L b_R^2 + a_R b_L^2) / D,  D = b_L^2 + b_R^2 - b_L^2 b_R^2,
+//   t_L = b_L (a_R - a_L (1 - b_R^2)) / D   (t_R likewise).
+// With invertible blocks this is the Sherman-Morrison step (b^2 = 1/(1+|v|^2),
+// a = alpha b^2); at a singular block b = 0 and nothing is divided by it.
+// D = 0 only if both blocks are singular at once (J loses rank): s is then the
+// mean of the two arms' values and t = 0 (not pinv's least-squares answer).
+template <typename T>
+IKG_HD inline void arm_minnorm7(const T (&A)[6][8], T* z, T* n, typename LaneT<T>::M* truncated = nullptr) {
+  // column order: 0 = chest (A[.][7]), 1..6 = arm joints (A[.][0..5]); row r
+  // of M keeps L's entries left of the diagonal and, from the diagonal on,
+  // the reflector v_r (L's diagonal goes to dg)
+  T M[6][7], dg[6], sc[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    M[r][0] = A[r][7];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) M[r][1 + k] = A[r][k];
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {  // H_r zeroes row r right of the diagonal (column operations)
+    T n2 = T(0);
+#pragma unroll
+    for (int j = r; j < 7; ++j) n2 += M[r][j] * M[r][j];
+    const T nrm = sqrt(n2);
+    const T arr = M[r][r];
+    dg[r] = vsel(arr >= T(0), -nrm, nrm);
+    M[r][r] = arr - dg[r];  // v_r = (row r from the diagonal) - dg e_r
+    const T vtv = T(2) * nrm * (nrm + fabs(arr));
+    sc[r] = vsel(vtv > T(0), fdiv(T(2), vtv), T(0));
+#pragma unroll
+    for (int i = r + 1; i < 6; ++i) {
+      T tau = T(0);
+#pragma unroll
+      for (int j = r; j < 7; ++j) tau += M[i][j] * M[r][j];
+      const T f = tau * sc[r];
+#pragma unroll
+      for (int j = r; j < 7; ++j) M[i][j] -= f * M[r][j];
+    }
+  }
+  // L y = e (lower triangular; pivots below rcond * max truncated, as pinv's)
+  T dmax = T(0);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dmax = fmax(dmax, fabs(dg[k]));
+  const T cut = dmax * T(Prec<T>::kRcond);
+  if (truncated) {
+    T dmin = fabs(dg[0]);
+#pragma unroll
+    for (int k = 1; k < 6; ++k) dmin = fmin(dmin, fabs(dg[k]));
+    *truncated = mnot(dmin > cut);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    T acc = A[k][6];
+#pragma unroll
+    for (int j = 0; j < k; ++j) acc -= M[k][j] * z[j];
+    z[k] = vsel(fabs(dg[k]) > cut, fdiv(acc, dg[k]), T(0));
+  }
+  z[6] = T(0);
+  // z = H_0 ... H_5 y, n = H_0 ... H_5 e_7
+#pragma unroll
+  for (int j = 0; j < 7; ++j) n[j] = j == 6 ? T(1) : T(0);
+#pragma unroll
+  for (int r = 5; r >= 0; --r) {
+    T dz = T(0), dn = T(0);
+#pragma unroll
+    for (int j = r; j < 7; ++j) {
+      dz += M[r][j] * z[j];
+      dn += M[r][j] * n[j];
+    }
+    dz *= sc[r];
+    dn *= sc[r];
+#pragma unroll
+    for (int j = r; j < 7; ++j) {
+      z[j] -= dz * M[r][j];
+      n[j] -= dn * M[r][j];
+    }
+  }
+}
+
+// The chest value s and this arm's null-space coefficient t from the two
+// arms' (a, b) (partner: ao, bo).  Both lanes of a pair must get the same s
+// bit for bit (each carries the chest joint), so every product is rounded on
+// its own (no contraction) and the sums are commutative.
+template <typename T>
+IKG_HD inline void minnorm_combine(T a, T b, T ao, T bo, T& s, T& t) {
+#pragma clang fp contract(off)
+  const T bb = b * b, bbo = bo * bo;
+  const T p = a * bbo, po = ao * bb;
+  const T num = p + po;
+  const T D = (bb + bbo) - bb * bbo;
+  const auto ok = D > T(Prec<T>::kRcond);
+  const T Ds = vsel(ok, D, T(1));
+  s = vsel(ok, fdiv(num, Ds), (a + ao) * T(0.5));
+  t = vsel(ok, fdiv(b * (ao - a * (T(1) - bbo)), Ds), T(0));
+}
+
+// pinv(J) e of the whole 12 x 13 system by one-sided (Hestenes) Jacobi on the
+// 12 rows of J, for the iterates where J itself loses rank (a straight elbow:
+// the chest cannot restore the lost direction; the LQ form then truncates a
+// pivot or D = 0).  np.linalg.pinv truncates singular values below
+// 1e-15 sigma_max (inverse_geometry.py:83); Jacobi's accurate small singular
+// values make the same cut.  Rows of J = [c | blockdiag(J_L, J_R)] come from
+// the two arm systems (arm_system layout); the rotations that orthogonalise
+// the rows are applied to e alongside, so x = sum_i w_i e~_i / sigma_i^2.
+// Output: x[0] chest, x[1..6] left arm, x[7..12] right arm.  Both lanes of a
+// pair run it on the same inputs in the same order: identical results.
+template <typename E>
+IKG_HD __attribute__((noinline)) void pinv_jacobi(const E (&AL)[6][8], const E (&AR)[6][8], E* x) {
+  // cold (rank-deficient J only): loops stay rolled so W lives in scratch
+  // memory instead of ~300 registers that would set the kernel's allocation
+  E W[12][13], e[12];
+#pragma nounroll
+  for (int r = 0; r < 6; ++r) {
+#pragma nounroll
+    for (int c = 0; c < 13; ++c) {
+      W[r][c] = E(0);
+      W[6 + r][c] = E(0);
+    }
+    W[r][0] = AL[r][7];
+    W[6 + r][0] = AR[r][7];
+#pragma nounroll
+    for (int k = 0; k < 6; ++k) {
+      W[r][1 + k] = AL[r][k];
+      W[6 + r][7 + k] = AR[r][k];
+    }
+    e[r] = AL[r][6];
+    e[6 + r] = AR[r][6];
+  }
+  const E tol = E(Prec<E>::kRcond);
+#pragma nounroll
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    bool rotated = false;
+#pragma nounroll
+    for (int i = 0; i < 11; ++i)
+#pragma nounroll
+      for (int j = i + 1; j < 12; ++j) {
+        E a = E(0), b = E(0), c = E(0);
+#pragma nounroll
+        for (int k = 0; k < 13; ++k) {
+          a += W[i][k] * W[i][k];
+          b += W[j][k] * W[j][k];
+          c += W[i][k] * W[j][k];
+        }
+        if (!(fabs(c) > tol * sqrt(a * b))) continue;
+        rotated = true;
+        const E zeta = (b - a) / (E(2) * c);
+        const E t = (zeta >= E(0) ? E(1) : E(-1)) / (fabs(zeta) + sqrt(E(1) + zeta * zeta));
+        const E cs = E(1) / sqrt(E(1) + t * t), sn = cs * t;
+#pragma nounroll
+        for (int k = 0; k < 13; ++k) {
+          const E wi = W[i][k], wj = W[j][k];
+          W[i][k] = cs * wi - sn * wj;
+          W[j][k] = sn * wi + cs * wj;
+        }
+        const E ei = e[i], ej = e[j];
+        e[i] = cs * ei - sn * ej;
+        e[j] = sn * ei + cs * ej;
+      }
+    if (!rotated) break;
+  }
+  E s2[12], smax = E(0);
+#pragma nounroll
+  for (int i = 0; i < 12; ++i) {
+    E a = E(0);
+#pragma nounroll
+    for (int k = 0; k < 13; ++k) a += W[i][k] * W[i][k];
+    s2[i] = a;
+    smax = fmax(smax, a);
+  }
+  const E cut2 = smax * E(Prec<E>::kRcond) * E(Prec<E>::kRcond);  // sigma_i > rcond sigma_max
+#pragma nounroll
+  for (int k = 0; k < 13; ++k) x[k] = E(0);
+#pragma nounroll
+  for (int i = 0; i < 12; ++i) {
+    if (!(s2[i] > cut2)) continue;
+    const E f = e[i] / s2[i];
+#pragma nounroll
+    for (int k = 0; k < 13; ++k) x[k] += W[i][k] * f;
+  }
+}
+
+// The 6 x 8 arm system in frame-1 axes at the hand point (the layout of
+// arm_system: columns 0..5 arm joints, 6 the error, 7 the chest), from the
+// frame-1 state (arm_fk_error_f1): axes a0 = e_z, a1 = a2 = e_y,
+// [a3 a4 a5] = Ry(q12) [e_x, Rx(q3) e_y, Rx(q3) Ry(q4) e_z]; the wrist axes
+// pass through w, the chest axis (e_z) through -(k, p0z).
+template <typename T, class SP>
+IKG_HD inline void arm_system_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
+                                 const T* sn, const T* cs, T (&A)[6][8]) {
+  const bool right = arm != 0;
+  const T* h = st.h;
+  T ax[7][3], org[7][3];
+  const T s3 = sn[4], c3 = cs[4], s4 = sn[5], c4 = cs[5], c12 = st.c12, s12 = st.s12;
+  // local wrist axes before Ry(q12): e_x, Rx(q3) e_y = (0, c3, s3), Rx(q3) Ry(q4) e_z = (s4, -s3 c4, c3 c4)
+  const T loc[3][3] = {{T(1), T(0), T(0)}, {T(0), c3, s3}, {s4, -s3 * c4, c3 * c4}};
+  const T ez[3] = {T(0), T(0), T(1)}, ey[3] = {T(0), T(1), T(0)};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    ax[0][i] = ez[i];  // chest
+    ax[1][i] = ez[i];
+    ax[2][i] = ey[i];
+    ax[3][i] = ey[i];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {  // Ry(q12) loc[k]
+    ax[4 + k][0] = c12 * loc[k][0] + s12 * loc[k][2];
+    ax[4 + k][1] = loc[k][1];
+    ax[4 + k][2] = c12 * loc[k][2] - s12 * loc[k][0];
+  }
+  const T p0z = SP::zero_t(0, 2) ? T(0) : armc<T>(right, m->arm_t[0][0][2], m->arm_t[1][0][2]);
+  org[0][0] = -st.k[0];
+  org[0][1] = -st.k[1];
+  org[0][2] = -p0z;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    org[1][i] = T(0);
+    org[2][i] = SP::zero_t(1, i) ? T(0) : armc<T>(right, m->arm_t[0][1][i], m->arm_t[1][1][i]);
+    org[3][i] = st.o2[i];
+    org[4][i] = st.w[i];
+    org[5][i] = st.w[i];
+    org[6][i] = st.w[i];
+  }
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const int col = j == 0 ? 7 : j - 1;
+    const T dx = h[0] - org[j][0], dy = h[1] - org[j][1], dz = h[2] - org[j][2];
+    A[0][col] = ax[j][1] * dz - ax[j][2] * dy;
+    A[1][col] = ax[j][2] * dx - ax[j][0] * dz;
+    A[2][col] = ax[j][0] * dy - ax[j][1] * dx;
+    A[3][col] = ax[j][0];
+    A[4][col] = ax[j][1];
+    A[5][col] = ax[j][2];
+  }
+#pragma unroll
+  for (int r = 0; r < 6; ++r) A[r][6] = st.e[r];
+}
+
 
 // lambda > 0: z_e, z_c = (J_a J_a^T + lambda I)^-1 [e_a, c_a]; alpha = c.z_e, beta = c.z_c.
 template <typename T>
@@ -1675,6 +1963,104 @@ IKG_HD inline void arm_dq_damped(const T (&A)[6][8], const T* ze, const T* zc, T
 #pragma unroll
     for (int r = 0; r < 6; ++r) acc += A[r][k] * y[r];
     dq[k] = acc;
+  }
+}
+
+// pinv(J) e for the pair (inverse_geometry.py:83): the closed-form
+// Sherman-Morrison step, and the LQ form (arm_minnorm7) for both lanes of a
+// pair when either arm block is near singular.  The guard travels in the sign
+// of the exchanged |v|^2 (never negative otherwise), so it costs no extra
+// exchange; both lanes of a pair take the branch together.
+struct PairX {  // the partner arm: lane ^ 1 (pair layout) or the other half (packed)
+  template <typename T>
+  __device__ T operator()(T x) const { return pair_swap(x); }
+};
+
+template <typename T, class X = PairX>
+__device__ inline void pinv_step_tail(const T* u, const T* v, T alpha, T beta, typename LaneT<T>::M bad, T* dq, T& s,
+                                      bool& need) {
+  const X xc;
+  const T btx = vsel(bad, T(-1), beta);
+  const T bo = xc(btx);
+  s = chest_step(alpha + xc(alpha), btx + bo);
+  arm_dq(u, v, s, dq);
+  need = any_of(mor(btx < T(0), bo < T(0)));
+}
+
+template <typename T, class X = PairX>
+__device__ inline void pinv_step_lq(const T (&A)[6][8], int arm, T* dq, T& s) {
+  using E = typename LaneT<T>::E;
+  const X xc;
+  T z[7], n[7], t;
+  typename LaneT<T>::M trunc;
+  arm_minnorm7(A, z, n, &trunc);
+  minnorm_combine(z[0], n[0], xc(z[0]), xc(n[0]), s, t);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) dq[k] = z[1 + k] + t * n[1 + k];
+  // J itself (nearly) rank deficient: a truncated pivot in either arm, or
+  // D = 0 in minnorm_combine (checked on both lanes alike)
+  const T bo = xc(n[0]), bb = n[0] * n[0], bbo = bo * bo;
+  const bool rank_def = any_of(mor(mor(trunc, mnot((bb + bbo) - bb * bbo > T(Prec<T>::kRcond))),
+                                   xc(vsel(trunc, T(1), T(0))) > T(0)));
+  if (rank_def) {
+    E AL[6][8], AR[6][8], x[13];
+    if constexpr (is_packed<T>) {
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          AL[r][c] = A[r][c].x;
+          AR[r][c] = A[r][c].y;
+        }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          const E mine = A[r][c], other = xc(A[r][c]);
+          AL[r][c] = arm ? other : mine;
+          AR[r][c] = arm ? mine : other;
+        }
+    }
+    pinv_jacobi(AL, AR, x);
+    if constexpr (is_packed<T>) {
+      s = T(x[0]);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) dq[k] = T{x[1 + k], x[7 + k]};
+    } else {
+      s = x[0];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) dq[k] = arm ? x[7 + k] : x[1 + k];
+    }
+  }
+}
+
+template <typename T, class SP, class X = PairX>
+__device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
+                                    const T* sn, const T* cs, T* dq, T& s) {
+  T u[6], v[6], alpha, beta;
+  typename LaneT<T>::M bad;
+  arm_solve_f1<T, SP>(m, arm, st, sn, cs, u, v, alpha, beta, &bad);
+  bool need;
+  pinv_step_tail<T, X>(u, v, alpha, beta, bad, dq, s, need);
+  if (__builtin_expect(need, 0)) {
+    T A[6][8];
+    arm_system_f1<T, SP>(m, arm, st, sn, cs, A);
+    pinv_step_lq<T, X>(A, arm, dq, s);
+  }
+}
+
+template <typename T, class SP>
+__device__ inline void pinv_step_cf(const ArmState<T>& st, int arm, T tau, T* dq, T& s) {
+  T u[6], v[6], alpha, beta;
+  typename LaneT<T>::M bad;
+  arm_solve<T, SP>(st, u, v, alpha, beta, &bad, tau);
+  bool need;
+  pinv_step_tail(u, v, alpha, beta, bad, dq, s, need);
+  if (__builtin_expect(need, 0)) {
+    T A[6][8];
+    arm_system(st, A);
+    pinv_step_lq(A, arm, dq, s);
   }
 }
 

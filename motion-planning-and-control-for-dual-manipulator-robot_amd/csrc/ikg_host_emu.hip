@@ -4,6 +4,7 @@
 // kernel's lanes execute them, so kernel numerics can be inspected without a
 // GPU.  Built as libikgrasp_emu.so; used by tests/test_host_emu.py.
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 
 #include "ikg_collision.hpp"
@@ -12,6 +13,10 @@
 #include "ikgrasp.h"
 
 namespace {
+
+// updates that took the LQ form (pinv_step_*), since the last ikg_emu_lq_count(1)
+thread_local long long lq_count = 0;
+thread_local long long svd_count = 0;  // of those, the 12 x 13 Jacobi form (pinv_jacobi)
 
 // collide_wave's stages run serially (same functions, same order per lane).
 template <typename T>
@@ -97,13 +102,14 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
         break;
       }
     }
-    T A[2][6][8], u[2][6], v[2][6], al[2], be[2], dq[6], q_old[2][7];
+    T A[2][6][8], u[2][6], v[2][6], al[2], be[2], dqa[2][6], sa[2], q_old[2][7];
+    bool bad[2] = {false, false};
     for (int arm = 0; arm < 2; ++arm) {
       q_old[arm][0] = qc[arm];
       for (int k = 0; k < kArmDof; ++k) q_old[arm][k + 1] = qa[arm][k];
       if constexpr (kFrame1<SP>) {
         if (f1) {
-          arm_solve_f1<T, SP>(&m, arm, s1[arm], sn[arm], cs[arm], u[arm], v[arm], al[arm], be[arm]);
+          arm_solve_f1<T, SP>(&m, arm, s1[arm], sn[arm], cs[arm], u[arm], v[arm], al[arm], be[arm], &bad[arm]);
           continue;
         }
       }
@@ -111,16 +117,50 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
         arm_system(st[arm], A[arm]);
         arm_solve_damped(A[arm], prm.lambda, u[arm], v[arm], al[arm], be[arm]);
       } else {
-        arm_solve<T, SP>(st[arm], u[arm], v[arm], al[arm], be[arm]);
+        arm_solve<T, SP>(st[arm], u[arm], v[arm], al[arm], be[arm], &bad[arm], m.sing_tau);
       }
+    }
+    for (int arm = 0; arm < 2; ++arm) {
+      sa[arm] = chest_step(al[arm] + al[1 - arm], be[arm] + be[1 - arm]);
+      if (damped)
+        arm_dq_damped(A[arm], u[arm], v[arm], sa[arm], dqa[arm]);
+      else
+        arm_dq(u[arm], v[arm], sa[arm], dqa[arm]);
+    }
+    if (!damped && (bad[0] || bad[1])) {  // pinv_step_f1 / pinv_step_cf: the LQ form for the pair
+      T z[2][7], n[2][7];
+      bool trunc[2];
+      for (int arm = 0; arm < 2; ++arm) {
+        if (f1) {
+          if constexpr (kFrame1<SP>) arm_system_f1<T, SP>(&m, arm, s1[arm], sn[arm], cs[arm], A[arm]);
+        } else {
+          arm_system(st[arm], A[arm]);
+        }
+        arm_minnorm7(A[arm], z[arm], n[arm], &trunc[arm]);
+      }
+      for (int arm = 0; arm < 2; ++arm) {
+        T t;
+        minnorm_combine(z[arm][0], n[arm][0], z[1 - arm][0], n[1 - arm][0], sa[arm], t);
+        for (int k = 0; k < 6; ++k) dqa[arm][k] = z[arm][1 + k] + t * n[arm][1 + k];
+      }
+      const T bb0 = n[0][0] * n[0][0], bb1 = n[1][0] * n[1][0];
+      if (trunc[0] || trunc[1] || !((bb0 + bb1) - bb0 * bb1 > T(Prec<T>::kRcond))) {  // pinv_jacobi
+        T x[13];
+        pinv_jacobi(A[0], A[1], x);
+        sa[0] = sa[1] = x[0];
+        for (int k = 0; k < 6; ++k) {
+          dqa[0][k] = x[1 + k];
+          dqa[1][k] = x[7 + k];
+        }
+        ++svd_count;
+      }
+      if (sa[0] != sa[1]) std::abort();  // both lanes must carry the same chest step
+      ++lq_count;
     }
     ++it;
     for (int arm = 0; arm < 2; ++arm) {
-      const T s = chest_step(al[arm] + al[1 - arm], be[arm] + be[1 - arm]);
-      if (damped)
-        arm_dq_damped(A[arm], u[arm], v[arm], s, dq);
-      else
-        arm_dq(u[arm], v[arm], s, dq);
+      const T s = sa[arm];
+      const T* dq = dqa[arm];
       ArmLimits<T> lim;
       load_limits(&m, arm, lim);
       arm_update(&m, arm, prm.dt, s, dq, qc[arm], qa[arm], IKG_LANE_LIMITS ? &lim : nullptr);
@@ -177,6 +217,17 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
 }
 
 }  // namespace
+
+extern "C" long long ikg_emu_lq_count(int reset) {
+  const long long v = lq_count;
+  if (reset) lq_count = 0;
+  return v;
+}
+extern "C" long long ikg_emu_svd_count(int reset) {
+  const long long v = svd_count;
+  if (reset) svd_count = 0;
+  return v;
+}
 
 // cd may be NULL; it is used when p->check_collision is set.
 extern "C" int ikg_emu_solve(const ikg_model_desc* d, int dtype, const void* targets, const void* q0,

@@ -38,10 +38,19 @@ namespace ikg {
 #ifndef IKG_WPE
 #define IKG_WPE 0
 #endif
+// Waves per SIMD the register allocation must leave room for: the guarded
+// step's LQ branch (pinv_step_f1) is cold, so spilling around it keeps the
+// loop at the occupancy it had without it (fp64 226 VGPRs: 2 waves; fp32
+// 103: 4); without the bound its registers took fp64 to 1 wave per SIMD.
+template <typename T, bool DAMPED, class SP>
+constexpr int kPairMinWaves = (kFrame1<SP> && !DAMPED) ? (sizeof(T) == 8 ? 2 : 4) : 1;
+
 template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
 __global__ __launch_bounds__(64)
 #if IKG_WPE
 __attribute__((amdgpu_waves_per_eu(1, IKG_WPE)))
+#else
+__attribute__((amdgpu_waves_per_eu(kPairMinWaves<T, DAMPED, SP>)))
 #endif
 void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             const T* __restrict__ targets,

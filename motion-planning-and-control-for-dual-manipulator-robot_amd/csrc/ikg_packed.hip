@@ -27,8 +27,11 @@ namespace ikg {
 // some kernels (after the collision continuation, 19-46 of 1,024 SIMDs held two
 // waves of the next 1,024-wave launch and the kernel took 2.2 ms instead of 1.4;
 // tools/placement_probe.py).  The launcher checks the resulting occupancy.
+// (amdgpu_waves_per_eu: the guarded step's cold LQ branch spills instead of
+// raising the allocation of the loop: 157 VGPRs, 3 waves per SIMD)
 template <class SP, int WPS, bool MED>
-__global__ __launch_bounds__(64) void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPS == 0 ? 3 : WPS)))
+void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               KParams<float> prm, const float* __restrict__ targets,
                                                               const float* __restrict__ q0, int64_t q0_stride,
                                                               int64_t B, int64_t S, float* __restrict__ q_out,

@@ -56,6 +56,11 @@ __device__ inline double x4(double x) {
 }
 __device__ inline float x4(float x) { return __int_as_float(x4_i32(__float_as_int(x))); }
 
+struct QuadX {  // the other arm's lane group (pinv_step_f1)
+  template <typename T>
+  __device__ T operator()(T x) const { return x4(x); }
+};
+
 template <typename T>
 __device__ inline T pick4(int r, T a, T b, T c, T d) {
   return r < 2 ? (r == 0 ? a : b) : (r == 2 ? c : d);
@@ -169,7 +174,8 @@ __device__ inline T quad_fk_error(const KModel<T>* __restrict__ m, int arm, int 
 }
 
 template <typename T, class SP>
-__global__ __launch_bounds__(64) void ikg_quad_batch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 8 ? 2 : 4)))
+void ikg_quad_batch_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                                                             const T* __restrict__ targets,
                                                             const T* __restrict__ q0, int64_t q0_stride, int64_t B,
                                                             int64_t S, T* __restrict__ q_out,
@@ -210,10 +216,8 @@ __global__ __launch_bounds__(64) void ikg_quad_batch_kernel(const KModel<T>* __r
     ThetaTrack<T>* tkp = (IKG_THETA_TRACK && is_f64<T>) ? &tk : nullptr;
     ArmStateF1<T> st;
     x = quad_fk_error<T, SP>(m, arm, j, sn, cs, RT, tT, st, tkp, (it % Trig<T>::kResync) == 0);
-    T u[6], v[6], alpha, beta, dq[6];
-    arm_solve_f1<T, SP>(m, arm, st, sn, cs, u, v, alpha, beta);
-    const T s = chest_step(alpha + x4(alpha), beta + x4(beta));
-    arm_dq(u, v, s, dq);
+    T dq[6], s;
+    pinv_step_f1<T, SP, QuadX>(m, arm, st, sn, cs, dq, s);
     xo = x4(x);
     if (it >= prm.max_iters) break;
     if (x < prm.eps2 && xo < prm.eps2) {  // |e_L| < eps and |e_R| < eps (:70)

@@ -134,18 +134,12 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     if constexpr (F1) {
       ArmStateF1<T> st;
       x = arm_fk_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, tkp, resync);
-      T u[6], v[6];
-      arm_solve_f1<T, SP>(m, arm, st, sn, cs, u, v, alpha, beta);
-      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
-      arm_dq(u, v, s, dq);
+      pinv_step_f1<T, SP>(m, arm, st, sn, cs, dq, s);
     } else {
     ArmState<T> st;
     x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, tkp, resync);
     if constexpr (!DAMPED) {
-      T u[6], v[6];
-      arm_solve<T, SP>(st, u, v, alpha, beta);
-      s = chest_step(alpha + pair_swap(alpha), beta + pair_swap(beta));
-      arm_dq(u, v, s, dq);
+      pinv_step_cf<T, SP>(st, arm, T(m->sing_tau), dq, s);
     } else {
       T A[6][8], ze[6], zc[6];
       arm_system(st, A);

@@ -220,13 +220,42 @@ def hand_errors(q, oMcubeL, oMcubeR, placements=None):
     return eL, eR
 
 
-def computeqgrasppose(q0, cube_R, cube_t, max_iters=MAX_ITERS, dt=DT, eps=EPSILON, lam=0.0):
+def pinv_exact(J, e, dps=40):
+    """pinv(J) e evaluated in dps-digit arithmetic on the float64 J and e, with
+    np.linalg.pinv's cut (singular values below 1e-15 sigma_max dropped), then
+    rounded to float64.  For the fixtures at arm singularities: where J is
+    ill-conditioned, np.linalg.pinv's own result carries ~eps * cond(J) of
+    LAPACK rounding (at cond(J) = 1.8e10 it puts 79 rad into the exactly-zero
+    head columns on the first step, tools/singular_probe.py); this is the
+    value it approximates.  Rank decisions come from a 40-digit SVD when
+    numpy's sigma_min / sigma_max < 1e-13, else the normal equations suffice
+    (cond(J)^2 << 10^dps)."""
+    import mpmath as mp
+    mp.mp.dps = dps
+    s = np.linalg.svd(J, compute_uv=False)
+    Jm = mp.matrix(J.tolist())
+    em = mp.matrix(list(map(float, e)))
+    if s[-1] < 1e-13 * s[0]:
+        U, S, V = mp.svd_r(Jm)
+        cut = mp.mpf("1e-15") * S[0]
+        x = mp.matrix(J.shape[1], 1)
+        for i in range(len(S)):
+            if S[i] > cut:
+                ui = U[:, i]
+                x += V[i, :].T * ((ui.T * em)[0] / S[i])
+    else:
+        x = Jm.T * mp.lu_solve(Jm * Jm.T, em)
+    return np.array([float(v) for v in x])
+
+
+def computeqgrasppose(q0, cube_R, cube_t, max_iters=MAX_ITERS, dt=DT, eps=EPSILON, lam=0.0, step=None):
     """Restatement of inverse_geometry.py:41-100 without the collision term.
 
     Returns (q, converged, iters, (|eL|, |eR|)) where `iters` is the number of
     joint updates applied (== index of the converged check).  `lam > 0`
     replaces pinv(J) e by J^T (J J^T + lam I)^-1 e — an extension the
-    reference does not have (parity for it is unpinned).
+    reference does not have (parity for it is unpinned).  `step(J, e)`
+    replaces np.linalg.pinv(J) @ e (e.g. pinv_exact).
     """
     placements = joint_placements()
     oMcubeL, oMcubeR = hook_targets(cube_R, cube_t)
@@ -242,6 +271,8 @@ def computeqgrasppose(q0, cube_R, cube_t, max_iters=MAX_ITERS, dt=DT, eps=EPSILO
         J = np.vstack([JL, JR])  # :80
         if lam > 0:
             vq = J.T @ np.linalg.solve(J @ J.T + lam * np.eye(12), e)
+        elif step is not None:
+            vq = step(J, e)
         else:
             vq = np.linalg.pinv(J) @ e  # :83
         q = q + vq * dt  # :86 pin.integrate on revolute joints

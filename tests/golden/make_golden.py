@@ -33,6 +33,10 @@
    states are those plus a seeded tracking error, plus 32 random states within
    the joint limits; outputs are the frame placements, velocities, J, dJ, dJ v
    in WORLD / LOCAL / LOCAL_WORLD_ALIGNED and the PD errors e, e_dot.
+9. `singular_cases.npz` — seeds at and near the arm-block singularities (wrist
+   c4 = 0, straight elbow, shoulder w_x = 0; offsets 0, 1e-9, 1e-6, 1e-3 rad)
+   solved by the numpy oracle and by the same loop with a 40-digit pinv step
+   (ik_oracle.pinv_exact), with cond(J) at the seed.
 8. `tilted_cube.urdf` + `generic_cases.npz` — the model-generality row (SURVEY
    §8f-3) on the synthetic tilted-axis robot `tilted_dualarm.urdf` (negative
    and unaligned joint axes, rotated placements; written for these tests):
@@ -116,6 +120,69 @@ def make_oracle_cases(n_uniform=48, n_yaw=24, n_seeded=24):
         err=np.array([[r[3], r[4]] for r in res]))
     print("wrote oracle_cases.npz:", {k: int((kind == k).sum()) for k in range(3)},
           "converged", sum(r[1] for r in res), "/", len(res))
+
+
+# Singular configurations of the arm blocks (round 3, tools/singular_probe.py),
+# found by root finding on the frame-1 geometry with every other joint at 0:
+# wrist c4 = 0 at LARM/RARM_JOINT4 = -pi/2; straight elbow det2 = 0 at
+# LARM/RARM_JOINT2 = ELBOW; shoulder w_x = 0 at LARM_JOINT1 = SHOULDER_L,
+# RARM_JOINT1 = SHOULDER_R (the root inside the right arm's limits).
+ELBOW = 1.4801364395941514
+SHOULDER_L = 0.8671825440154443
+SHOULDER_R = -2.2744101095743487
+SING_DELTAS = (0.0, 1e-9, 1e-6, 1e-3)
+
+
+def _solve_sing(args):
+    target, q0, exact = args
+    R, t = target[:9].reshape(3, 3), target[9:]
+    q, ok, it, (nl, nr) = ik_oracle.computeqgrasppose(q0, R, t)
+    qx, okx, itx, (nlx, nrx) = ik_oracle.computeqgrasppose(q0, R, t, step=ik_oracle.pinv_exact) if exact else \
+        (q, ok, it, (nl, nr))
+    oL, oR = ik_oracle.hook_targets(R, t)
+    J = np.vstack([ik_oracle.frame_jacobian_local(q0, ik_oracle.FRAME_LEFT),
+                   ik_oracle.frame_jacobian_local(q0, ik_oracle.FRAME_RIGHT)])
+    s = np.linalg.svd(J, compute_uv=False)
+    return q, ok, it, nl, nr, qx, okx, itx, nlx, nrx, s[0] / s[-1]
+
+
+def make_singular_cases():
+    """Seeds at and near the arm-block singularities (wrist, straight elbow,
+    shoulder) x two targets each (uniform sampler; +-45 deg yaw), solved by the
+    numpy oracle (np.linalg.pinv, the reference's step) and by the same loop
+    with the step in 40-digit arithmetic (ik_oracle.pinv_exact).  Where
+    cond(J) is large (the straight elbow: the chest cannot restore the lost
+    direction), the two differ by numpy's rounding; elsewhere they agree."""
+    seeds, kind, arm, delta = [], [], [], []
+    for d in SING_DELTAS:
+        for a, (jw, je, js, vs) in enumerate(((7, 5, 4, SHOULDER_L), (13, 11, 10, SHOULDER_R))):
+            for k, (j, v) in enumerate(((jw, -np.pi / 2), (je, ELBOW), (js, vs))):
+                q = np.zeros(15)
+                q[j] = v + d
+                seeds.append(q)
+                kind.append(k)
+                arm.append(a)
+                delta.append(d)
+    n = len(seeds)
+    t_u = uniform_targets(n, seed=110)
+    t_y = uniform_targets(n, seed=111, yaw=np.pi / 4)
+    targets = np.concatenate([t_u, t_y])
+    q0 = np.concatenate([seeds, seeds])
+    kind = np.array(kind * 2, dtype=np.int8)
+    with Pool(8) as p:
+        res = p.map(_solve_sing, [(t, q, True) for t, q in zip(targets, q0)])
+    np.savez_compressed(
+        os.path.join(HERE, "singular_cases.npz"),
+        targets=targets, q0=q0, kind=kind, arm=np.array(arm * 2, dtype=np.int8), delta=np.array(delta * 2),
+        q=np.array([r[0] for r in res]), converged=np.array([r[1] for r in res]),
+        iters=np.array([r[2] for r in res], dtype=np.int32), err=np.array([[r[3], r[4]] for r in res]),
+        q_exact=np.array([r[5] for r in res]), converged_exact=np.array([r[6] for r in res]),
+        iters_exact=np.array([r[7] for r in res], dtype=np.int32),
+        err_exact=np.array([[r[8], r[9]] for r in res]), cond0=np.array([r[10] for r in res]))
+    dq = np.abs(np.array([r[0] for r in res]) - np.array([r[5] for r in res])).max(axis=1)
+    print("wrote singular_cases.npz:", n * 2, "cases; converged", sum(r[1] for r in res),
+          "; numpy vs exact pinv |dq| max", float(dq.max()), "at cond0",
+          float(np.array([r[10] for r in res])[dq.argmax()]))
 
 
 _SCENE = None
@@ -403,3 +470,5 @@ if __name__ == "__main__":
         make_control_cases()
     if "generic" in what:
         make_generic_cases()
+    if "singular" in what:
+        make_singular_cases()
