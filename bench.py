@@ -3,21 +3,34 @@
     python bench.py [--gpus N --steps K --warmup W --batch B --dtype f64|f32]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`--gpus N > 1` without a launcher (WORLD_SIZE unset) starts the N rank
+processes itself (a child `torch.distributed.run`, one rank per GPU); with
+fewer GPUs than ranks it rehearses over gloo (ranks share the devices,
+collectives on host copies) and says so in `config.parallelism`.
+
 A step = one launch of the batched IK kernel over this rank's batch of
 synthetic grasp targets (already resident in HBM) plus, for N > 1, the RCCL
 gather of the final q to rank 0 (north star: "at most an RCCL gather of the
 final q over xGMI").  Weak scaling: every rank solves `--batch` targets.
-Default workload = BASELINE.json configs[1]: 4,096 targets, fp64, 1 GPU.
+Default workload = BASELINE.json configs[1]: 4,096 targets, fp64.
 
 `value` counts CONVERGED solves per second over all ranks (the metric's
 unit); all problems/s is reported beside it.  The dominant kernel's roofline
 is VALU (fp64/fp32 vector ALU, no MFMA, negligible HBM traffic) — see
-DESIGN.md §5; the HBM figure the north star asks for is reported as
-`roofline_hbm`.
+DESIGN.md §5; the HBM figure the north star asks for is `roofline_hbm`.
+
+The same JSON line carries, under `extra` (timed after the headline):
+  * `c4_strong`: BASELINE configs[3], 1,048,576 targets split over the ranks
+    (strong scaling), each step the shard solves plus the RCCL gather of q,
+    flags and update counts to rank 0 (ikgrasp.parallel);
+  * `c2_collision`: configs[1] with the reference's `success` (the collision
+    term of inverse_geometry.py:70, :97-98), with its own roofline and CPU leg.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,9 +40,165 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd"))
 
 METRIC = "grasp-pose IK solves/sec (Nextage dual-arm) at 1/2/4/8 MI355X"
-F_ITER = 3144  # FP ops per IK iteration
-PEAK_VALU = {"f64": 78.6, "f32": 157.3}  # TFLOP/s vector peaks (MI355X spec)
+F_ITER = 3144  # FP ops per IK iteration of the reference formulation
+# Vector (VALU) peaks, TFLOP/s: fp32 from MI355X_MICROARCH.md (157.3); fp64 is
+# AMD's MI355X spec-sheet figure (78.6), not listed in the guide
+PEAK_VALU = {"f64": 78.6, "f32": 157.3}
 PEAK_HBM = 8000.0  # GB/s (MI355X_MICROARCH.md)
+C4_TOTAL = 1 << 20  # BASELINE configs[3]
+
+
+# ---------------------------------------------------------------- host / CPU
+def cpu_share():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU
+    quota (the GPU box gives a job a share of a large host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    return max(1, min(n, int(quota)) if quota else n), quota
+
+
+def host_cpus():
+    """(model name, logical CPUs, physical cores) of the host."""
+    model, cores = None, set()
+    phys = core = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                k, _, v = ln.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and model is None:
+                    model = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif not k and phys is not None and core is not None:
+                    cores.add((phys, core))
+                    phys = core = None
+    except OSError:
+        pass
+    if phys is not None and core is not None:
+        cores.add((phys, core))
+    return model, os.cpu_count(), len(cores) or None
+
+
+def cpu_baseline(targets, budget_s=10.0, numpy_budget_s=8.0):
+    """The reference-semantics CPU loop on this host, beside the GPU run:
+    (1) the C restatement (oracle/ikg_oracle.c, OpenMP, one problem per
+    thread) on every CPU this job may use, ~budget_s of work over the
+    benchmark's own targets (repeated); (2) the numpy oracle
+    (oracle/ik_oracle.py: the reference-shaped loop, np.linalg.pinv) on one
+    core over a prefix of the targets.  The host's full core count is stated
+    with a per-core extrapolation; the measured value is what ran."""
+    sys.path.insert(0, ROOT)
+    from oracle import c_oracle, ik_oracle
+    threads, quota = cpu_share()
+    if os.environ.get("IKG_CPU_THREADS"):
+        threads = int(os.environ["IKG_CPU_THREADS"])
+    n_cal = min(len(targets), 8 * threads)
+    t0 = time.perf_counter()
+    c_oracle.solve(targets[:n_cal], np.zeros(15), threads=threads)
+    per = (time.perf_counter() - t0) / n_cal
+    n = int(max(n_cal, budget_s / max(per, 1e-9)))
+    reps = -(-n // len(targets))
+    sample = np.concatenate([targets] * reps)[:n] if reps > 1 else targets[:n]
+    t0 = time.perf_counter()
+    _, conv, iters, _ = c_oracle.solve(sample, np.zeros(15), threads=threads)
+    dt = time.perf_counter() - t0
+    model, logical, physical = host_cpus()
+    value = float(conv.sum() / dt)
+    # numpy single core: whole solves until the budget is spent
+    t0, k, nconv = time.perf_counter(), 0, 0
+    while time.perf_counter() - t0 < numpy_budget_s and k < len(targets):
+        t = targets[k]
+        _, ok, _, _ = ik_oracle.computeqgrasppose(np.zeros(15), t[:9].reshape(3, 3), t[9:])
+        nconv += bool(ok)
+        k += 1
+    dn = time.perf_counter() - t0
+    return {
+        "value": value, "unit": "converged solves/s", "cores": threads, "kind": "port",
+        "sample": f"{n} solves = the {len(targets)} benchmark targets x {n / len(targets):.2f}, q0=0, fp64 C "
+                  f"restatement (oracle/ikg_oracle.c, OpenMP, {threads} threads), {dt:.1f} s; "
+                  f"all-problem rate {n / dt:.1f}/s",
+        "cpu_model": model, "host_logical_cpus": logical, "host_physical_cores": physical,
+        "job_cpu_share": quota, "threads_used": threads,
+        "per_thread_converged_per_s": value / threads,
+        "all_physical_cores_extrapolated": (value / threads * physical) if physical else None,
+        "numpy_single_core": {
+            "value": nconv / dn, "unit": "converged solves/s", "cores": 1, "kind": "port",
+            "sample": f"first {k} benchmark targets, oracle/ik_oracle.py (np.linalg.pinv per update), {dn:.1f} s, "
+                      f"{nconv} converged; {k / dn:.2f} problems/s"},
+    }
+
+
+def cpu_baseline_collision(targets, scene_json, budget_s=8.0):
+    """The reference-semantics loop WITH the collision term (the C collision
+    restatement in oracle/ikg_oracle.c, checked against
+    tests/golden/collision_cases.npz), on every CPU this job may use, over
+    the same scene the GPU run uses."""
+    sys.path.insert(0, ROOT)
+    from oracle import c_oracle, collision_oracle
+    if not c_oracle.has_collision():
+        return None
+    sc = collision_oracle.prepare(json.loads(scene_json))
+    threads, _ = cpu_share()
+    if os.environ.get("IKG_CPU_THREADS"):
+        threads = int(os.environ["IKG_CPU_THREADS"])
+    n_cal = min(len(targets), 4 * threads)
+    t0 = time.perf_counter()
+    c_oracle.solve_collision(sc, targets[:n_cal], np.zeros(15), threads=threads)
+    per = (time.perf_counter() - t0) / n_cal
+    n = int(max(n_cal, budget_s / max(per, 1e-9)))
+    reps = -(-n // len(targets))
+    sample = np.concatenate([targets] * reps)[:n] if reps > 1 else targets[:n]
+    t0 = time.perf_counter()
+    _, ok, _, _ = c_oracle.solve_collision(sc, sample, np.zeros(15), threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": float(ok.sum() / dt), "unit": "collision-free converged solves/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{n} solves of the benchmark targets, q0=0, fp64 C restatement with the collision term "
+                      f"(oracle/ikg_oracle.c), {dt:.1f} s"}
+
+
+# ---------------------------------------------------------------- roofline inputs
+def flops_profile(kernel, dtype, med):
+    """Executed FP operations per problem-update of a kernel (rocprofv3 VALU
+    instruction counters, tools/pmc_flops.py) -> (ops, source) or None."""
+    names = [f"flops_{kernel}_{dtype}{'_med' if med else ''}.json"]
+    if kernel == "pair" and not med:
+        names.append(f"flops_{dtype}_b4096.json")  # round-2 name
+    for n in names:
+        p = os.path.join(ROOT, "profiles", n)
+        if os.path.exists(p):
+            with open(p) as f:
+                return json.load(f)["fp_ops_per_problem_iter"], os.path.relpath(p, ROOT)
+    return None
+
+
+def hbm_profile(dtype, B, S=0, collision=False):
+    """Counter HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE) for this
+    configuration, from profiles/pmc_*.json, or None."""
+    tag = f"pmc_{dtype}_b{B}" + (f"_s{S}" if S else "") + ("_col" if collision else "") + ".json"
+    p = os.path.join(ROOT, "profiles", tag)
+    if os.path.exists(p):
+        with open(p) as f:
+            return json.load(f).get("hbm_bytes_per_launch"), os.path.relpath(p, ROOT)
+    return None, None
 
 
 def algorithmic_bytes(dtype, B, nq=15, broadcast_q0=True):
@@ -49,38 +218,62 @@ def multistart_bytes(dtype, T, S, nq=15):
     return T * per_target + S * nq * s + T * S * per_problem
 
 
-def cpu_baseline(targets, budget_s=10.0):
-    """Time the C restatement (oracle/ikg_oracle.c) on host cores over a
-    bounded prefix of the same workload."""
-    sys.path.insert(0, ROOT)
-    from oracle import c_oracle
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = min(threads, 16)
-    n_cal = min(len(targets), 8 * threads)
-    t0 = time.perf_counter()
-    c_oracle.solve(targets[:n_cal], np.zeros(15), threads=threads)
-    per = (time.perf_counter() - t0) / n_cal
-    # ~budget_s of CPU work: the benchmark targets, repeated as often as needed
-    n = int(max(n_cal, budget_s / max(per, 1e-9)))
-    reps = -(-n // len(targets))
-    sample = np.concatenate([targets] * reps)[:n] if reps > 1 else targets[:n]
-    t0 = time.perf_counter()
-    _, conv, iters, _ = c_oracle.solve(sample, np.zeros(15), threads=threads)
-    dt = time.perf_counter() - t0
-    cpu_model = None
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), None)
-    except OSError:
-        pass
-    return {
-        "value": float(conv.sum() / dt), "unit": "converged solves/s", "cores": threads, "kind": "port",
-        "cpu_model": cpu_model, "host_cpus": os.cpu_count(),
-        "sample": f"{n} solves = the {len(targets)} benchmark targets x {n / len(targets):.2f}, q0=0, fp64 C "
-                  f"restatement (oracle/ikg_oracle.c, OpenMP), {dt:.1f} s; all-problem rate {n / dt:.1f}/s",
+def roofline(dtype, kernel, med, kern_ms, sum_iters, waves, simds, abytes, traffic, traffic_src):
+    """The dominant kernel's VALU roofline (SURVEY count and executed count)
+    and its HBM figures (algorithmic bytes and counter bytes)."""
+    survey = (sum_iters * F_ITER) / (kern_ms * 1e-3) / 1e12 if sum_iters else None
+    ex = flops_profile(kernel, dtype, med)
+    executed = None
+    if ex and sum_iters:
+        a = sum_iters * ex[0] / (kern_ms * 1e-3) / 1e12
+        executed = {"fp_ops_per_problem_iter": ex[0], "achieved": a, "frac": a / PEAK_VALU[dtype],
+                    "unit": "TFLOP/s", "waves": waves, "simds": simds, "source": ex[1]}
+    frac = survey / PEAK_VALU[dtype] if survey else None
+    out = {
+        "bound": "valu", "achieved": survey, "peak": PEAK_VALU[dtype], "unit": "TFLOP/s", "frac": frac,
+        "traffic": traffic, "kernel_ms": kern_ms,
+        "work": f"sum(updates)={sum_iters} x {F_ITER} FP ops (SURVEY §8a reference formulation)",
+        "executed": executed,
     }
+    if frac and frac > 1:
+        out["note"] = ("frac > 1: the kernel's closed-form frame-1 loop executes fewer FP ops than the "
+                       "reference formulation it is priced at (see executed)")
+    hbm = {"bound": "hbm", "algorithmic_bytes": abytes,
+           "algorithmic_GBps": abytes / (kern_ms * 1e-3) / 1e9, "peak": PEAK_HBM, "unit": "GB/s",
+           "traffic": traffic, "traffic_source": traffic_src}
+    if traffic:
+        hbm["achieved"] = traffic / (kern_ms * 1e-3) / 1e9
+        hbm["frac"] = hbm["achieved"] / PEAK_HBM
+    else:
+        hbm["achieved"] = hbm["algorithmic_GBps"]
+        hbm["frac"] = hbm["achieved"] / PEAK_HBM
+        hbm["achieved_is"] = "algorithmic bytes (no counter profile for this configuration)"
+    return out, hbm
 
 
+# ---------------------------------------------------------------- launcher
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """--gpus N without a launcher: N rank processes under a child
+    torch.distributed.run (not an exec of this process).  Fewer GPUs than
+    ranks: a gloo rehearsal (ranks share devices; not a throughput number)."""
+    import torch
+    env = dict(os.environ)
+    ndev = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if ndev < n and "IKG_BENCH_BACKEND" not in env:
+        env["IKG_BENCH_BACKEND"] = "gloo"
+        print(f"[bench] {n} ranks on {ndev} GPU(s): gloo rehearsal", file=sys.stderr)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=env)
+
+
+# ---------------------------------------------------------------- GPU side
 class QGather:
     """The per-step gather of the final q to rank 0 (north star: "at most an
     RCCL gather of the final q over xGMI").  Device collectives (RCCL): step
@@ -122,6 +315,45 @@ class QGather:
                 self.pending[i] = None
 
 
+def timed(torch, dist, world, steps, warmup, step, stream, drain=None):
+    """warmup untimed steps, then `steps` timed ones bracketed by a barrier
+    and synchronize; returns (this rank's wall s, mean kernel ms) where the
+    kernel time is HIP events on the launch stream around each solve.
+    `drain` completes outstanding collectives inside the timed region."""
+    for _ in range(warmup):
+        step(None)
+    if drain:
+        drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(events[k])
+    if drain:
+        drain()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    return elapsed, float(np.mean([a.elapsed_time(b) for a, b in events]))
+
+
+def reduce_stats(torch, dist, world, host, dev, vals, n_max):
+    """[max over ranks of the first n_max values] + [sum of the rest]."""
+    t = torch.tensor(vals, dtype=torch.float64, device="cpu" if host else dev)
+    if world > 1:
+        mx = t[:n_max].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t[n_max:].clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        t = torch.cat([mx, sm])
+    return t.tolist()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -132,15 +364,18 @@ def main():
     ap.add_argument("--yaw", type=float, default=0.0, help="random yaw range (rad) of the cube targets")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the c4_strong / c2_collision extras")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--multistart", type=int, default=0,
                     help="seeds per target (BASELINE configs[4]): every target solved from S random seeds, "
                          "best seed kept; value counts converged targets/s")
     ap.add_argument("--collision", action="store_true",
-                    help="reference `success` with the collision term (inverse_geometry.py:70, :97-98): "
-                         "converged-but-colliding problems iterate on in the continuation kernel; "
-                         "value counts collision-free converged solves/s")
+                    help="reference `success` with the collision term (inverse_geometry.py:70, :97-98) as the "
+                         "headline; value counts collision-free converged solves/s")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -152,26 +387,26 @@ def main():
     # fewer GPUs than ranks (ranks share devices, collectives on host copies);
     # the measured configuration is RCCL ("nccl"), one rank per GPU
     backend = os.environ.get("IKG_BENCH_BACKEND", "nccl")
+    ndev = max(1, torch.cuda.device_count())
     if backend == "gloo":
-        local = local % max(1, torch.cuda.device_count())
+        local = local % ndev
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()  # what the communicator saw
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     host = backend != "nccl"  # collectives on host copies
 
     from ikgrasp import _lib
+    from ikgrasp.collision import load_nextage_scene
+    from ikgrasp.parallel import gather_rows, shard_range
     from ikgrasp.solver import IKSolver
     from ikgrasp.workload import random_seeds, uniform_targets
 
-    scene = None
-    if args.collision:
-        from ikgrasp.collision import load_nextage_scene
-        scene = load_nextage_scene()
-    solver = IKSolver(device=local, scene=scene)
+    solver = IKSolver(device=local, scene=load_nextage_scene())
     B = args.batch
     tg_np = uniform_targets(B, seed=rank, yaw=args.yaw)
     tdt = torch.float64 if args.dtype == "f64" else torch.float32
@@ -195,7 +430,7 @@ def main():
 
     gather = QGather(dist, q_out, gathered, world, enabled=not args.no_gather, host=host)
 
-    def step(ev=None):
+    def step(ev):
         qb = gather.buffer()
         if ev is not None:
             ev[0].record(stream)
@@ -209,24 +444,7 @@ def main():
             ev[1].record(stream)
         gather.submit(qb)
 
-    for _ in range(args.warmup):
-        step()
-    gather.drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(events[k])
-    gather.drain()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    elapsed, kern_ms = timed(torch, dist, world, args.steps, args.warmup, step, stream, drain=gather.drain)
 
     n_conv = int(conv.sum().item())
     sum_iters = int(iters.to(torch.int64).sum().item())
@@ -246,47 +464,41 @@ def main():
         torch.cuda.synchronize()
         sum_iters = int(i_x.to(torch.int64).sum().item())
         del tg_x, q0_x, q_x, c_x, i_x, e_x
-    stats = torch.tensor([elapsed, kern_ms, n_conv, B, sum_iters], dtype=torch.float64,
-                         device="cpu" if host else dev)
-    if world > 1:
-        t_max = stats[:2].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        counts = stats[2:].clone()
-        dist.all_reduce(counts, op=dist.ReduceOp.SUM)
-        stats = torch.cat([t_max, counts])
-    elapsed, kern_ms, tot_conv, tot_B, tot_iters = stats.tolist()
+    elapsed, kern_ms, tot_conv, tot_B, tot_iters = reduce_stats(
+        torch, dist, world, host, dev, [elapsed, kern_ms, n_conv, B, sum_iters], 2)
 
     # the batch kernel the C-ABI dispatches (ikg_kernels.hip launch_pair_batch): the packed fp32
     # layout from B >= 65,536 on 256 CUs (2 pair waves per SIMD), else the pair layout
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    # (multi-start: AUTO keeps the pair layout)
     packed = args.dtype == "f32" and (args.variant == _lib.IKG_VARIANT_PACKED or
                                       (args.variant == _lib.IKG_VARIANT_AUTO and not S and B > cus * 4 * 32))
     kname = "ikg_packed_batch_kernel" if packed else "ikg_pair_batch_kernel"
     layout = "packed layout (both arms per lane, 64 problems/wave)" if packed else "pair layout (2 lanes/problem)"
+    ppw = 64 if packed else 32
+
+    extra = {}
+    if not args.no_extra and not S and not args.collision:
+        extra = run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, stream, sh, gather_rows,
+                           shard_range, uniform_targets)
+
     if rank == 0:
         per_step = elapsed / args.steps
         value = tot_conv / per_step
-        flops = (sum_iters * F_ITER) / (kern_ms * 1e-3) / 1e12 if sum_iters else None  # rank-0 kernel, TFLOP/s
         abytes = algorithmic_bytes(args.dtype, B) if not S else multistart_bytes(args.dtype, B, S)
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", f"pmc_{args.dtype}_b{B}.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        # executed FP ops per problem-iteration of this kernel (rocprofv3 FMA/MUL/ADD/TRANS counters,
-        # tools/pmc_flops.py): the frame-1 loop does ~1/3 of the reference formulation's 3,144, so the
-        # SURVEY-count frac above overstates hardware use; executed_frac is the hardware VALU fraction
-        executed = None
-        fl = os.path.join(ROOT, "profiles", f"flops_{args.dtype}_b{B}.json")
-        if os.path.exists(fl) and kname == "ikg_pair_batch_kernel" and sum_iters:
-            with open(fl) as f:
-                per_it = json.load(f)["fp_ops_per_problem_iter"]
-            ex = sum_iters * per_it / (kern_ms * 1e-3) / 1e12
-            waves = -(-B // 32)
-            executed = {"fp_ops_per_problem_iter": per_it, "achieved": ex, "frac": ex / PEAK_VALU[args.dtype],
-                        "unit": "TFLOP/s", "waves": waves, "simds": cus * 4,
-                        "source": os.path.relpath(fl, ROOT)}
+        traffic, tsrc = hbm_profile(args.dtype, B, S, args.collision)
+        rl, rl_hbm = roofline(args.dtype, "packed" if packed else "pair", bool(S), kern_ms, sum_iters,
+                              -(-B * max(S, 1) // ppw), cus * 4, abytes, traffic, tsrc)
+        if args.collision:
+            rl["kernel"] = kname + " (records every iterate past the first passing one) + ikg_prescreen_kernel + " \
+                                   "ikg_traj_scan_kernel"
+            rl["kernel_ms_covers"] = "the whole solve: batch kernel, pre-screen, compaction, record scan"
+        else:
+            rl["kernel"] = kname
+        parallelism = f"shard{world}"
+        if world > 1:
+            parallelism += "" if args.no_gather else ("+rccl_gather_q" if not host else "+gloo_gather_q")
+            if host:
+                parallelism += " (gloo rehearsal: ranks share GPUs, not a throughput number)"
         out = {
             "metric": METRIC, "value": value, "unit": "converged solves/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": per_step * 1e3,
@@ -295,39 +507,116 @@ def main():
             "config": {
                 "workload": (f"BASELINE configs[4]: multi-start {S} seeds x {B} targets per GPU, {args.dtype}"
                              if S else
-                             f"BASELINE configs[1]: batch {B} grasp targets per GPU, {args.dtype}, "
-                             f"{layout}") +
-                            (" + collision term (continuation kernel)" if args.collision else ""),
+                             f"BASELINE configs[1]: batch {B} grasp targets per GPU, {args.dtype}, {layout}") +
+                            (" + collision term" if args.collision else ""),
                 "collision_term": bool(args.collision),
                 "seeds_per_target": S or 1,
                 "batch_per_gpu": B, "global_batch": B * world, "yaw_range": args.yaw,
-                "parallelism": f"shard{world}" + ("" if world == 1 or args.no_gather else
-                                                  ("+rccl_gather_q" if not host else "+gloo_gather_q")),
+                "parallelism": parallelism, "world_size_seen": world, "backend": backend if world > 1 else None,
+                "devices_visible": ndev,
             },
             "problems_per_s": tot_B / per_step,
             "converged_fraction": tot_conv / tot_B,
             "mean_iters": (tot_iters / tot_B) if not S else None,
             "mean_iters_all_problems": (tot_iters / (tot_B * S)) if S else None,
-            "roofline": {
-                "bound": "valu", "achieved": flops, "peak": PEAK_VALU[args.dtype], "unit": "TFLOP/s",
-                "frac": flops / PEAK_VALU[args.dtype] if flops else None, "traffic": traffic,
-                "kernel": kname + (" + ikg_collide_continue_kernel" if args.collision else ""),
-                "kernel_ms": kern_ms,
-                "work": f"sum(iters)={sum_iters} x {F_ITER} FP ops (SURVEY §8a)",
-                "executed": executed,
-            },
-            "roofline_hbm": {
-                "bound": "hbm", "achieved": abytes / (kern_ms * 1e-3) / 1e9, "peak": PEAK_HBM, "unit": "GB/s",
-                "frac": abytes / (kern_ms * 1e-3) / 1e9 / PEAK_HBM, "traffic": traffic,
-                "algorithmic_bytes": abytes,
-            },
+            "roofline": rl,
+            "roofline_hbm": rl_hbm,
         }
         if world == 1 and not args.no_cpu_baseline and not S and not args.collision:
             out["cpu_baseline"] = cpu_baseline(tg_np)
+        if extra:
+            if world == 1 and not args.no_cpu_baseline and "c2_collision" in extra:
+                extra["c2_collision"]["cpu_baseline"] = cpu_baseline_collision(tg_np, solver.scene.to_json())
+            out["extra"] = extra
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
     solver.close()
+
+
+def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, stream, sh, gather_rows, shard_range,
+               uniform_targets):
+    """The c4_strong and c2_collision figures (see the module docstring)."""
+    from ikgrasp import _lib
+    extra = {}
+    # ---- C4: 1,048,576 targets split over the ranks, gather of q / flags / iters to rank 0
+    tot = C4_TOTAL
+    lo, hi = shard_range(tot, rank, world)
+    all_t = uniform_targets(tot, seed=7)
+    n = hi - lo
+    tg4 = torch.tensor(all_t[lo:hi], dtype=torch.float64, device=dev)
+    del all_t
+    q04 = torch.zeros(15, dtype=torch.float64, device=dev)
+    q4 = torch.empty((n, 15), dtype=torch.float64, device=dev)
+    c4 = torch.empty(n, dtype=torch.uint8, device=dev)
+    i4 = torch.empty(n, dtype=torch.int32, device=dev)
+    e4 = torch.empty((n, 2), dtype=torch.float64, device=dev)
+
+    def step4(ev):
+        if ev is not None:
+            ev[0].record(stream)
+        solver.solve_into(tg4, q04, q4, c4, i4, e4, _lib.IKG_F64, sh)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            for t in (q4, c4, i4):
+                gather_rows(t.cpu() if host else t, tot, dst=0)
+
+    steps4 = max(3, min(args.steps, 5))
+    el4, km4 = timed(torch, dist, world, steps4, 1, step4, stream)
+    el4, km4, conv4, it4 = reduce_stats(torch, dist, world, host, dev,
+                                        [el4, km4, int(c4.sum().item()), int(i4.to(torch.int64).sum().item())], 2)
+    del tg4, q4, c4, i4, e4
+    if rank == 0:
+        ps = el4 / steps4
+        extra["c4_strong"] = {
+            "workload": f"BASELINE configs[3]: {tot} targets (uniform_targets seed 7) split over {world} rank(s), "
+                        "fp64, pair layout; each step the shard solves plus the gather of q, flags and update "
+                        "counts to rank 0" + (" (RCCL)" if world > 1 and not host else
+                                               " (gloo rehearsal)" if world > 1 else ""),
+            "value": conv4 / ps, "unit": "converged solves/s", "problems_per_s": tot / ps,
+            "ms_per_step": ps * 1e3, "kernel_ms_max_rank": km4, "scaling": "strong", "n_gpus": world,
+            "steps": steps4, "converged_fraction": conv4 / tot,
+            "roofline_survey_frac": it4 * F_ITER / (km4 * 1e-3) / 1e12 / PEAK_VALU["f64"] / world,
+        }
+    # ---- C2 with the collision term (the reference's success)
+    B = args.batch
+    tg = torch.tensor(uniform_targets(B, seed=rank), dtype=torch.float64, device=dev)
+    q0 = torch.zeros(15, dtype=torch.float64, device=dev)
+    qc = torch.empty((B, 15), dtype=torch.float64, device=dev)
+    cc = torch.empty(B, dtype=torch.uint8, device=dev)
+    ic = torch.empty(B, dtype=torch.int32, device=dev)
+    ec = torch.empty((B, 2), dtype=torch.float64, device=dev)
+
+    def stepc(ev):
+        if ev is not None:
+            ev[0].record(stream)
+        solver.solve_into(tg, q0, qc, cc, ic, ec, _lib.IKG_F64, sh, check_collision=True)
+        if ev is not None:
+            ev[1].record(stream)
+
+    elc, kmc = timed(torch, dist, world, args.steps, args.warmup, stepc, stream)
+    elc, kmc, convc, itc = reduce_stats(torch, dist, world, host, dev,
+                                        [elc, kmc, int(cc.sum().item()), int(ic.to(torch.int64).sum().item())], 2)
+    if rank == 0:
+        ps = elc / args.steps
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        traffic, tsrc = hbm_profile("f64", B, 0, True)
+        rl, rl_hbm = roofline("f64", "pair", False, kmc, int(itc), -(-B // 32), cus * 4,
+                              algorithmic_bytes("f64", B) + 48 * 8 * 12, traffic, tsrc)
+        rl["kernel"] = ("ikg_pair_batch_kernel (records every iterate past the first passing one) + "
+                        "ikg_prescreen_kernel + ikg_traj_scan_kernel")
+        rl["kernel_ms_covers"] = "the whole solve (all its kernels)"
+        rl["work"] += " -- the updates the reference runs; checks are not priced"
+        extra["c2_collision"] = {
+            "workload": f"BASELINE configs[1] with the reference's success (collision term, "
+                        f"inverse_geometry.py:70, :97-98): batch {B} per GPU, fp64",
+            "value": convc / ps, "unit": "collision-free converged solves/s", "ms_per_step": ps * 1e3,
+            "kernel_ms": kmc, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "converged_fraction": convc / (B * world), "mean_iters": itc / (B * world),
+            "roofline": rl, "roofline_hbm": rl_hbm,
+        }
+    return extra
 
 
 if __name__ == "__main__":

@@ -682,7 +682,7 @@ __device__ __forceinline__ T cont_step(const KModel<T>* __restrict__ m, const KP
     x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st);
   T alpha, beta;
   if constexpr (!DAMPED) {
-    pinv_step_cf<T, SP>(st, arm, m->sing_tau, dq, s);
+    pinv_step_cf<T, SP>(st, arm, m->sing_tau, m->sing_beta, dq, s);
   } else {
     T A[6][8], ze[6], zc[6];
     arm_system(st, A);

@@ -58,15 +58,40 @@
 #define IKG_THETA_ASIN 1
 #endif
 
-// Relative tolerance of the singularity guard (pinv_step): an arm block whose
-// closed-form inverse scale exceeds 1/tau takes the LQ form.  fp64: the
-// closed form's error grows like ~6e-19/delta at a wrist offset delta from
-// the singular angle (tools/singular_probe.py), 1e-6 keeps it below 1e-12.
+// The singularity guard of the closed-form step (pinv_step_*).  The closed
+// form dq_a = u_a - s v_a (v_a = J_a^-1 c_a, s ~ |u| / |v|) rounds to
+// ~eps |v_a| relative to the step: the cancellation grows with |v|, i.e.
+// where the chest column has a component along the direction the arm block
+// loses.  That is the wrist (c4 -> 0) and the shoulder (w_x -> 0), where J
+// itself stays well conditioned (cond ~ 1e2) and pinv does not blow up: the
+// pair then takes the per-arm pinv form.  At a straight elbow the chest cannot restore
+// the lost direction, |v| stays moderate and J itself is ill conditioned, so
+// the closed form is as accurate as any pinv (both ~eps cond(J)) until J is
+// rank deficient to rounding, where v (and the guard) blows up and the
+// branch's per-arm pinv truncates as np.linalg.pinv does (arm_pinv7).  The guard is one
+// integer compare of |v|^2 (bits, so an inf/NaN from an exactly singular
+// block's reciprocal also trips it) against sing_beta: fp64 1e14 (the step's
+// relative rounding stays below ~1e-9 per update and the KAT-style final q
+// within ~1e-11 of pinv, tools/singular_probe.py), fp32 1e12.  Tighter
+// bounds trip on unconverged problems that wander near the wrist for
+// hundreds of updates (C5-style random seeds: 630 of 505,859 fp64 updates at
+// 1e10, 17 at 1e14), stalling their waves.
+// Timing knob: IKG_SING_GUARD=0 builds the unguarded closed form.
+#ifndef IKG_SING_GUARD
+#define IKG_SING_GUARD 1
+#endif
+#ifndef IKG_SING_BETA64
+#define IKG_SING_BETA64 1e14
+#endif
+#ifndef IKG_SING_BETA32
+#define IKG_SING_BETA32 1e12f
+#endif
+// generic-path (chest frame, Householder / 3 x 3 adjugate) relative pivot bound
 #ifndef IKG_SING_TAU64
-#define IKG_SING_TAU64 1e-6
+#define IKG_SING_TAU64 1e-7
 #endif
 #ifndef IKG_SING_TAU32
-#define IKG_SING_TAU32 1e-3
+#define IKG_SING_TAU32 1e-4
 #endif
 
 namespace ikg {
@@ -110,12 +135,10 @@ struct KModel {
   T jt[kMaxNq][3];
   int32_t jaxis[kMaxNq];
   int32_t jparent[kMaxNq];
-  // singularity guard of the closed-form arm solve (pinv_step, build_kmodel):
-  // relative tolerance tau of this precision, and tau * L, tau * L^2 with L the
-  // arm's shoulder-to-wrist link length sum (shoulder: |w_x|, elbow: |det2|)
+  // singularity guard (pinv_step_*, build_kmodel): the bound on |v_a|^2 of
+  // the closed form, and the generic path's relative pivot bound
+  T sing_beta;
   T sing_tau;
-  T sing_wx[2];
-  T sing_det2[2];
 };
 
 // ---------------------------------------------------------------- kernel specialisation
@@ -1596,8 +1619,7 @@ IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__
 // inv3_apply2.
 template <typename T, class SP>
 IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
-                                const T* sn, const T* cs, T* u, T* v, T& alpha, T& beta,
-                                typename LaneT<T>::M* near_singular = nullptr) {
+                                const T* sn, const T* cs, T* u, T* v, T& alpha, T& beta) {
   const bool right = arm != 0;
   const T* w = st.w;
   const T* ev = st.e;
@@ -1618,7 +1640,9 @@ IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__
   }
   const T det2 = P1[0] * P2[2] - P1[2] * P2[0];
   const T dG = w[0] * det2;
-  const T rG = vsel<T>(dG != T(0), frcp(dG), T(0));
+  // an exactly singular block gives inf / NaN here; the guard (pinv_step_f1,
+  // on the bits of |v|^2) sends it to the per-arm pinv form
+  const T rG = frcp(dG);
   const T iP0 = det2 * rG, iD = w[0] * rG;
   {
     u[0] = bl[1] * iP0;
@@ -1634,7 +1658,7 @@ IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__
   }
   // H = Ry(q12) H''; slots 4, 5 = arm joints 3, 4
   const T s3 = sn[4], c3 = cs[4], s4 = sn[5], c4 = cs[5];
-  const T rH = vsel<T>(c4 != T(0), frcp(c4), T(0));
+  const T rH = frcp(c4);
   const T c4r = c4 * rH;
   const T c12 = st.c12, s12 = st.s12;
   {  // e: z = Ry(q12)^T (e_w - (0, x1 + x2, x0))
@@ -1658,201 +1682,168 @@ IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__
     alpha += u[k] * v[k];
     beta += v[k] * v[k];
   }
-  if (near_singular) {  // shoulder (w_x), elbow (det2) or wrist (c4) below the guard (pinv_step)
-    const T twx = armc<T>(right, m->sing_wx[0], m->sing_wx[1]);
-    const T tdet = armc<T>(right, m->sing_det2[0], m->sing_det2[1]);
-    *near_singular = mor(mor(fabs(w[0]) < twx, fabs(det2) < tdet), fabs(c4) < T(m->sing_tau));
-  }
 }
+
+// The guard's test: x beyond the bound, or inf / NaN (compared as unsigned
+// bits, which -ffinite-math-only cannot fold away; x >= 0 or NaN here).
+IKG_HD inline bool beyond(double x, double b) {
+  return __builtin_bit_cast(uint64_t, x) > __builtin_bit_cast(uint64_t, b);
+}
+IKG_HD inline bool beyond(float x, float b) {
+  return __builtin_bit_cast(uint32_t, x) > __builtin_bit_cast(uint32_t, b);
+}
+IKG_HD inline v2i beyond(v2f x, float b) { return v2i{beyond(x.x, b) ? -1 : 0, beyond(x.y, b) ? -1 : 0}; }
 
 // ---------------------------------------------------------------- singular arm blocks
 // pinv(J) e for J = [c | blockdiag(J_L, J_R)] without inverting the arm
 // blocks, for the iterates where one of them is (nearly) singular.  Per arm,
-// M_a = [c_a | J_a] (6 x 7) has full row rank even when J_a does not; with
-// z_a its minimum-norm solution of M_a z = e_a and n_a its unit null vector
-// (Householder LQ), the solutions sharing the chest value s are
-// z_a + t_a n_a, s = a_a + t_a b_a (a = z[0], b = n[0]), and
-//   min  s^2 + |x_L|^2 + |x_R|^2 = |z_L|^2 + |z_R|^2 - s^2
+// M_a = [c_a | J_a] (6 x 7).  With z_a = M_a^+ e_a (minimum-norm least
+// squares) and p_a = P_null(M_a) e_0 = e_0 - M_a^+ c_a (the chest axis e_0
+// projected on M_a's null space, bb_a = p_a[0] = |p_a|^2), the least-squares
+// solutions of the arm's rows with chest value s are z_a + p_a t_a + (null
+// directions without a chest component), s = a_a + bb_a t_a (a = z_a[0]),
+// and pinv's minimum of s^2 + |x_L|^2 + |x_R|^2 = |z_L|^2 + |z_R|^2 - s^2 + ...
 // over them is attained at
-//   s = (a_L b_R^2 + a_R b_L^2) / D,  D = b_L^2 + b_R^2 - b_L^2 b_R^2,
-//   t_L = b_L (a_R - a_L (1 - b_R^2)) / D   (t_R likewise).
-// With invertible blocks this is the Sherman-Morrison step (b^2 = 1/(1+|v|^2),
-// a = alpha b^2); at a singular block b = 0 and nothing is divided by it.
-// D = 0 only if both blocks are singular at once (J loses rank): s is then the
-// mean of the two arms' values and t = 0 (not pinv's least-squares answer).
+//   s = (a_L bb_R + a_R bb_L) / D,  D = bb_L + bb_R - bb_L bb_R,
+//   z_L + p_L (a_R - a_L (1 - bb_R)) / D   (the right arm likewise).
+// With invertible blocks this is the Sherman-Morrison step (bb = 1/(1+|v|^2),
+// a = alpha bb).  A block that loses rank even with the chest column (a
+// straight elbow) has bb = 0 and pins s; its least-squares z_a is pinv's.
+// D = 0 only if both arms pin s (J loses rank through the coupling): s is then
+// the mean of the two values (not pinv's least-squares compromise).
+//
+// M_a^+ by one-sided (Hestenes) Jacobi on M_a's 6 rows: rotations G make the
+// rows w_i orthogonal, M^+ b = sum_i w_i (G b)_i / |w_i|^2 over the rows with
+// |w_i| > 1e-15 max |w|, np.linalg.pinv's cut (Jacobi's small singular values
+// are accurate, so the rank decision is pinv's).  Both right-hand sides (e, c)
+// are rotated along.
+// sqrt in the lane type's own precision (the global ::sqrt would take a float
+// through double)
 template <typename T>
-IKG_HD inline void arm_minnorm7(const T (&A)[6][8], T* z, T* n, typename LaneT<T>::M* truncated = nullptr) {
-  // column order: 0 = chest (A[.][7]), 1..6 = arm joints (A[.][0..5]); row r
-  // of M keeps L's entries left of the diagonal and, from the diagonal on,
-  // the reflector v_r (L's diagonal goes to dg)
-  T M[6][7], dg[6], sc[6];
+IKG_HD inline T tsqrt(T x) {
+  if constexpr (is_packed<T> || is_f64<T>)
+    return sqrt(x);
+  else
+    return sqrtf(x);
+}
+
+template <typename T>
+IKG_HD inline T tabs(T x) {
+  if constexpr (is_packed<T> || is_f64<T>)
+    return fabs(x);
+  else
+    return fabsf(x);
+}
+template <typename T>
+IKG_HD inline T tmax(T x, T y) {
+  if constexpr (is_packed<T> || is_f64<T>)
+    return fmax(x, y);
+  else
+    return fmaxf(x, y);
+}
+
+#ifdef IKG_SING_COUNT
+// diagnostic build: [0] lanes that took the branch, [1] Jacobi sweeps (per TU)
+static __device__ unsigned long long g_sing[4];
+#define IKG_SING_TALLY(k, n) atomicAdd(&g_sing[k], (unsigned long long)(n))
+#else
+#define IKG_SING_TALLY(k, n) ((void)0)
+#endif
+
+template <typename T>
+IKG_HD inline void arm_pinv7(const T (&A)[6][8], T* z, T* p) {
+  using E = typename LaneT<T>::E;
+  // column order: 0 = chest (A[.][7]), 1..6 = arm joints (A[.][0..5])
+  T W[6][7], e[6], c[6];
 #pragma unroll
   for (int r = 0; r < 6; ++r) {
-    M[r][0] = A[r][7];
+    W[r][0] = A[r][7];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) M[r][1 + k] = A[r][k];
+    for (int k = 0; k < 6; ++k) W[r][1 + k] = A[r][k];
+    e[r] = A[r][6];
+    c[r] = A[r][7];
+  }
+  const T tol = T(E(Prec<E>::kRcond));
+#pragma nounroll
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    bool rotated = false;
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+#pragma unroll
+      for (int j = i + 1; j < 6; ++j) {
+        T a = T(0), b = T(0), d = T(0);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          a += W[i][k] * W[i][k];
+          b += W[j][k] * W[j][k];
+          d += W[i][k] * W[j][k];
+        }
+        const auto rot = tabs(d) > tol * tsqrt(a * b);
+        rotated |= any_of(rot);
+        const T dd = vsel(rot, d, T(1));
+        const T zeta = fdiv(b - a, T(2) * dd);
+        const T t = fdiv(vsel(zeta >= T(0), T(1), T(-1)), tabs(zeta) + tsqrt(T(1) + zeta * zeta));
+        const T cs = vsel(rot, fdiv(T(1), tsqrt(T(1) + t * t)), T(1));
+        const T sn = vsel(rot, cs * t, T(0));
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          const T wi = W[i][k], wj = W[j][k];
+          W[i][k] = cs * wi - sn * wj;
+          W[j][k] = sn * wi + cs * wj;
+        }
+        const T ei = e[i], ej = e[j], ci = c[i], cj = c[j];
+        e[i] = cs * ei - sn * ej;
+        e[j] = sn * ei + cs * ej;
+        c[i] = cs * ci - sn * cj;
+        c[j] = sn * ci + cs * cj;
+      }
+#if defined(IKG_SING_COUNT) && defined(__HIP_DEVICE_COMPILE__)
+    IKG_SING_TALLY(1, 1);
+#endif
+    if (!rotated) break;
+  }
+  T s2[6], smax = T(0);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    T a = T(0);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) a += W[i][k] * W[i][k];
+    s2[i] = a;
+    smax = tmax(smax, a);
+  }
+  const T cut2 = smax * tol * tol;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    z[k] = T(0);
+    p[k] = k == 0 ? T(1) : T(0);
   }
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {  // H_r zeroes row r right of the diagonal (column operations)
-    T n2 = T(0);
+  for (int i = 0; i < 6; ++i) {
+    const auto keep = s2[i] > cut2;
+    const T r = vsel(keep, fdiv(T(1), vsel(keep, s2[i], T(1))), T(0));
+    const T fe = e[i] * r, fc = c[i] * r;
 #pragma unroll
-    for (int j = r; j < 7; ++j) n2 += M[r][j] * M[r][j];
-    const T nrm = sqrt(n2);
-    const T arr = M[r][r];
-    dg[r] = vsel(arr >= T(0), -nrm, nrm);
-    M[r][r] = arr - dg[r];  // v_r = (row r from the diagonal) - dg e_r
-    const T vtv = T(2) * nrm * (nrm + fabs(arr));
-    sc[r] = vsel(vtv > T(0), fdiv(T(2), vtv), T(0));
-#pragma unroll
-    for (int i = r + 1; i < 6; ++i) {
-      T tau = T(0);
-#pragma unroll
-      for (int j = r; j < 7; ++j) tau += M[i][j] * M[r][j];
-      const T f = tau * sc[r];
-#pragma unroll
-      for (int j = r; j < 7; ++j) M[i][j] -= f * M[r][j];
-    }
-  }
-  // L y = e (lower triangular; pivots below rcond * max truncated, as pinv's)
-  T dmax = T(0);
-#pragma unroll
-  for (int k = 0; k < 6; ++k) dmax = fmax(dmax, fabs(dg[k]));
-  const T cut = dmax * T(Prec<T>::kRcond);
-  if (truncated) {
-    T dmin = fabs(dg[0]);
-#pragma unroll
-    for (int k = 1; k < 6; ++k) dmin = fmin(dmin, fabs(dg[k]));
-    *truncated = mnot(dmin > cut);
-  }
-#pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    T acc = A[k][6];
-#pragma unroll
-    for (int j = 0; j < k; ++j) acc -= M[k][j] * z[j];
-    z[k] = vsel(fabs(dg[k]) > cut, fdiv(acc, dg[k]), T(0));
-  }
-  z[6] = T(0);
-  // z = H_0 ... H_5 y, n = H_0 ... H_5 e_7
-#pragma unroll
-  for (int j = 0; j < 7; ++j) n[j] = j == 6 ? T(1) : T(0);
-#pragma unroll
-  for (int r = 5; r >= 0; --r) {
-    T dz = T(0), dn = T(0);
-#pragma unroll
-    for (int j = r; j < 7; ++j) {
-      dz += M[r][j] * z[j];
-      dn += M[r][j] * n[j];
-    }
-    dz *= sc[r];
-    dn *= sc[r];
-#pragma unroll
-    for (int j = r; j < 7; ++j) {
-      z[j] -= dz * M[r][j];
-      n[j] -= dn * M[r][j];
+    for (int k = 0; k < 7; ++k) {
+      z[k] += W[i][k] * fe;
+      p[k] -= W[i][k] * fc;
     }
   }
 }
 
-// The chest value s and this arm's null-space coefficient t from the two
-// arms' (a, b) (partner: ao, bo).  Both lanes of a pair must get the same s
+// The chest value s and this arm's coefficient f (z_a + p_a f) from the two
+// arms' (a, bb) (partner: ao, bbo).  Both lanes of a pair must get the same s
 // bit for bit (each carries the chest joint), so every product is rounded on
 // its own (no contraction) and the sums are commutative.
 template <typename T>
-IKG_HD inline void minnorm_combine(T a, T b, T ao, T bo, T& s, T& t) {
+IKG_HD inline void minnorm_combine(T a, T bb, T ao, T bbo, T& s, T& f) {
 #pragma clang fp contract(off)
-  const T bb = b * b, bbo = bo * bo;
-  const T p = a * bbo, po = ao * bb;
-  const T num = p + po;
+  const T pr = a * bbo, po = ao * bb;
+  const T num = pr + po;
   const T D = (bb + bbo) - bb * bbo;
   const auto ok = D > T(Prec<T>::kRcond);
   const T Ds = vsel(ok, D, T(1));
   s = vsel(ok, fdiv(num, Ds), (a + ao) * T(0.5));
-  t = vsel(ok, fdiv(b * (ao - a * (T(1) - bbo)), Ds), T(0));
-}
-
-// pinv(J) e of the whole 12 x 13 system by one-sided (Hestenes) Jacobi on the
-// 12 rows of J, for the iterates where J itself loses rank (a straight elbow:
-// the chest cannot restore the lost direction; the LQ form then truncates a
-// pivot or D = 0).  np.linalg.pinv truncates singular values below
-// 1e-15 sigma_max (inverse_geometry.py:83); Jacobi's accurate small singular
-// values make the same cut.  Rows of J = [c | blockdiag(J_L, J_R)] come from
-// the two arm systems (arm_system layout); the rotations that orthogonalise
-// the rows are applied to e alongside, so x = sum_i w_i e~_i / sigma_i^2.
-// Output: x[0] chest, x[1..6] left arm, x[7..12] right arm.  Both lanes of a
-// pair run it on the same inputs in the same order: identical results.
-template <typename E>
-IKG_HD __attribute__((noinline)) void pinv_jacobi(const E (&AL)[6][8], const E (&AR)[6][8], E* x) {
-  // cold (rank-deficient J only): loops stay rolled so W lives in scratch
-  // memory instead of ~300 registers that would set the kernel's allocation
-  E W[12][13], e[12];
-#pragma nounroll
-  for (int r = 0; r < 6; ++r) {
-#pragma nounroll
-    for (int c = 0; c < 13; ++c) {
-      W[r][c] = E(0);
-      W[6 + r][c] = E(0);
-    }
-    W[r][0] = AL[r][7];
-    W[6 + r][0] = AR[r][7];
-#pragma nounroll
-    for (int k = 0; k < 6; ++k) {
-      W[r][1 + k] = AL[r][k];
-      W[6 + r][7 + k] = AR[r][k];
-    }
-    e[r] = AL[r][6];
-    e[6 + r] = AR[r][6];
-  }
-  const E tol = E(Prec<E>::kRcond);
-#pragma nounroll
-  for (int sweep = 0; sweep < 30; ++sweep) {
-    bool rotated = false;
-#pragma nounroll
-    for (int i = 0; i < 11; ++i)
-#pragma nounroll
-      for (int j = i + 1; j < 12; ++j) {
-        E a = E(0), b = E(0), c = E(0);
-#pragma nounroll
-        for (int k = 0; k < 13; ++k) {
-          a += W[i][k] * W[i][k];
-          b += W[j][k] * W[j][k];
-          c += W[i][k] * W[j][k];
-        }
-        if (!(fabs(c) > tol * sqrt(a * b))) continue;
-        rotated = true;
-        const E zeta = (b - a) / (E(2) * c);
-        const E t = (zeta >= E(0) ? E(1) : E(-1)) / (fabs(zeta) + sqrt(E(1) + zeta * zeta));
-        const E cs = E(1) / sqrt(E(1) + t * t), sn = cs * t;
-#pragma nounroll
-        for (int k = 0; k < 13; ++k) {
-          const E wi = W[i][k], wj = W[j][k];
-          W[i][k] = cs * wi - sn * wj;
-          W[j][k] = sn * wi + cs * wj;
-        }
-        const E ei = e[i], ej = e[j];
-        e[i] = cs * ei - sn * ej;
-        e[j] = sn * ei + cs * ej;
-      }
-    if (!rotated) break;
-  }
-  E s2[12], smax = E(0);
-#pragma nounroll
-  for (int i = 0; i < 12; ++i) {
-    E a = E(0);
-#pragma nounroll
-    for (int k = 0; k < 13; ++k) a += W[i][k] * W[i][k];
-    s2[i] = a;
-    smax = fmax(smax, a);
-  }
-  const E cut2 = smax * E(Prec<E>::kRcond) * E(Prec<E>::kRcond);  // sigma_i > rcond sigma_max
-#pragma nounroll
-  for (int k = 0; k < 13; ++k) x[k] = E(0);
-#pragma nounroll
-  for (int i = 0; i < 12; ++i) {
-    if (!(s2[i] > cut2)) continue;
-    const E f = e[i] / s2[i];
-#pragma nounroll
-    for (int k = 0; k < 13; ++k) x[k] += W[i][k] * f;
-  }
+  f = vsel(ok, fdiv(ao - a * (T(1) - bbo), Ds), T(0));
 }
 
 // The 6 x 8 arm system in frame-1 axes at the hand point (the layout of
@@ -1967,7 +1958,7 @@ IKG_HD inline void arm_dq_damped(const T (&A)[6][8], const T* ze, const T* zc, T
 }
 
 // pinv(J) e for the pair (inverse_geometry.py:83): the closed-form
-// Sherman-Morrison step, and the LQ form (arm_minnorm7) for both lanes of a
+// Sherman-Morrison step, and the per-arm pinv form (arm_pinv7) for both lanes of a
 // pair when either arm block is near singular.  The guard travels in the sign
 // of the exchanged |v|^2 (never negative otherwise), so it costs no extra
 // exchange; both lanes of a pair take the branch together.
@@ -1977,73 +1968,36 @@ struct PairX {  // the partner arm: lane ^ 1 (pair layout) or the other half (pa
 };
 
 template <typename T, class X = PairX>
-__device__ inline void pinv_step_tail(const T* u, const T* v, T alpha, T beta, typename LaneT<T>::M bad, T* dq, T& s,
-                                      bool& need) {
+__device__ inline void pinv_step_tail(const T* u, const T* v, T alpha, T beta, typename LaneT<T>::E bound, T* dq,
+                                      T& s, bool& need) {
   const X xc;
-  const T btx = vsel(bad, T(-1), beta);
-  const T bo = xc(btx);
-  s = chest_step(alpha + xc(alpha), btx + bo);
+  const T bo = xc(beta);
+  s = chest_step(alpha + xc(alpha), beta + bo);
   arm_dq(u, v, s, dq);
-  need = any_of(mor(btx < T(0), bo < T(0)));
+  need = any_of(mor(beyond(beta, bound), beyond(bo, bound)));
 }
 
 template <typename T, class X = PairX>
-__device__ inline void pinv_step_lq(const T (&A)[6][8], int arm, T* dq, T& s) {
-  using E = typename LaneT<T>::E;
+__device__ inline void pinv_step_lq(const T (&A)[6][8], int, T* dq, T& s) {
   const X xc;
-  T z[7], n[7], t;
-  typename LaneT<T>::M trunc;
-  arm_minnorm7(A, z, n, &trunc);
-  minnorm_combine(z[0], n[0], xc(z[0]), xc(n[0]), s, t);
+  T z[7], p[7], f;
+#ifdef IKG_SING_COUNT
+  IKG_SING_TALLY(0, 1);
+#endif
+  arm_pinv7(A, z, p);
+  minnorm_combine(z[0], p[0], xc(z[0]), xc(p[0]), s, f);
 #pragma unroll
-  for (int k = 0; k < 6; ++k) dq[k] = z[1 + k] + t * n[1 + k];
-  // J itself (nearly) rank deficient: a truncated pivot in either arm, or
-  // D = 0 in minnorm_combine (checked on both lanes alike)
-  const T bo = xc(n[0]), bb = n[0] * n[0], bbo = bo * bo;
-  const bool rank_def = any_of(mor(mor(trunc, mnot((bb + bbo) - bb * bbo > T(Prec<T>::kRcond))),
-                                   xc(vsel(trunc, T(1), T(0))) > T(0)));
-  if (rank_def) {
-    E AL[6][8], AR[6][8], x[13];
-    if constexpr (is_packed<T>) {
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          AL[r][c] = A[r][c].x;
-          AR[r][c] = A[r][c].y;
-        }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          const E mine = A[r][c], other = xc(A[r][c]);
-          AL[r][c] = arm ? other : mine;
-          AR[r][c] = arm ? mine : other;
-        }
-    }
-    pinv_jacobi(AL, AR, x);
-    if constexpr (is_packed<T>) {
-      s = T(x[0]);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) dq[k] = T{x[1 + k], x[7 + k]};
-    } else {
-      s = x[0];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) dq[k] = arm ? x[7 + k] : x[1 + k];
-    }
-  }
+  for (int k = 0; k < 6; ++k) dq[k] = z[1 + k] + f * p[1 + k];
 }
 
 template <typename T, class SP, class X = PairX>
 __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
                                     const T* sn, const T* cs, T* dq, T& s) {
   T u[6], v[6], alpha, beta;
-  typename LaneT<T>::M bad;
-  arm_solve_f1<T, SP>(m, arm, st, sn, cs, u, v, alpha, beta, &bad);
+  arm_solve_f1<T, SP>(m, arm, st, sn, cs, u, v, alpha, beta);
   bool need;
-  pinv_step_tail<T, X>(u, v, alpha, beta, bad, dq, s, need);
-  if (__builtin_expect(need, 0)) {
+  pinv_step_tail<T, X>(u, v, alpha, beta, m->sing_beta, dq, s, need);
+  if (__builtin_expect(IKG_SING_GUARD && need, 0)) {
     T A[6][8];
     arm_system_f1<T, SP>(m, arm, st, sn, cs, A);
     pinv_step_lq<T, X>(A, arm, dq, s);
@@ -2051,13 +2005,15 @@ __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restri
 }
 
 template <typename T, class SP>
-__device__ inline void pinv_step_cf(const ArmState<T>& st, int arm, T tau, T* dq, T& s) {
+__device__ inline void pinv_step_cf(const ArmState<T>& st, int arm, T tau, T bound, T* dq, T& s) {
   T u[6], v[6], alpha, beta;
   typename LaneT<T>::M bad;
   arm_solve<T, SP>(st, u, v, alpha, beta, &bad, tau);
   bool need;
-  pinv_step_tail(u, v, alpha, beta, bad, dq, s, need);
-  if (__builtin_expect(need, 0)) {
+  // a small relative pivot (truncated by the QR, or a small 3 x 3
+  // determinant) travels as an out-of-bound |v|^2
+  pinv_step_tail(u, v, alpha, vsel(bad, T(3e38), beta), bound, dq, s, need);
+  if (__builtin_expect(IKG_SING_GUARD && need, 0)) {
     T A[6][8];
     arm_system(st, A);
     pinv_step_lq(A, arm, dq, s);

@@ -16,7 +16,7 @@ namespace {
 
 // updates that took the LQ form (pinv_step_*), since the last ikg_emu_lq_count(1)
 thread_local long long lq_count = 0;
-thread_local long long svd_count = 0;  // of those, the 12 x 13 Jacobi form (pinv_jacobi)
+thread_local long long svd_count = 0;  // of those, with an arm that pins the chest (bb = 0: rank-deficient M_a)
 
 // collide_wave's stages run serially (same functions, same order per lane).
 template <typename T>
@@ -109,7 +109,8 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
       for (int k = 0; k < kArmDof; ++k) q_old[arm][k + 1] = qa[arm][k];
       if constexpr (kFrame1<SP>) {
         if (f1) {
-          arm_solve_f1<T, SP>(&m, arm, s1[arm], sn[arm], cs[arm], u[arm], v[arm], al[arm], be[arm], &bad[arm]);
+          arm_solve_f1<T, SP>(&m, arm, s1[arm], sn[arm], cs[arm], u[arm], v[arm], al[arm], be[arm]);
+          bad[arm] = beyond(be[arm], m.sing_beta);
           continue;
         }
       }
@@ -118,6 +119,7 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
         arm_solve_damped(A[arm], prm.lambda, u[arm], v[arm], al[arm], be[arm]);
       } else {
         arm_solve<T, SP>(st[arm], u[arm], v[arm], al[arm], be[arm], &bad[arm], m.sing_tau);
+        bad[arm] = bad[arm] || beyond(be[arm], m.sing_beta);
       }
     }
     for (int arm = 0; arm < 2; ++arm) {
@@ -127,35 +129,24 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
       else
         arm_dq(u[arm], v[arm], sa[arm], dqa[arm]);
     }
-    if (!damped && (bad[0] || bad[1])) {  // pinv_step_f1 / pinv_step_cf: the LQ form for the pair
-      T z[2][7], n[2][7];
-      bool trunc[2];
+    if (!damped && (bad[0] || bad[1])) {  // pinv_step_f1 / pinv_step_cf: the per-arm pinv form
+      T z[2][7], pv[2][7];
       for (int arm = 0; arm < 2; ++arm) {
         if (f1) {
           if constexpr (kFrame1<SP>) arm_system_f1<T, SP>(&m, arm, s1[arm], sn[arm], cs[arm], A[arm]);
         } else {
           arm_system(st[arm], A[arm]);
         }
-        arm_minnorm7(A[arm], z[arm], n[arm], &trunc[arm]);
+        arm_pinv7(A[arm], z[arm], pv[arm]);
       }
       for (int arm = 0; arm < 2; ++arm) {
-        T t;
-        minnorm_combine(z[arm][0], n[arm][0], z[1 - arm][0], n[1 - arm][0], sa[arm], t);
-        for (int k = 0; k < 6; ++k) dqa[arm][k] = z[arm][1 + k] + t * n[arm][1 + k];
-      }
-      const T bb0 = n[0][0] * n[0][0], bb1 = n[1][0] * n[1][0];
-      if (trunc[0] || trunc[1] || !((bb0 + bb1) - bb0 * bb1 > T(Prec<T>::kRcond))) {  // pinv_jacobi
-        T x[13];
-        pinv_jacobi(A[0], A[1], x);
-        sa[0] = sa[1] = x[0];
-        for (int k = 0; k < 6; ++k) {
-          dqa[0][k] = x[1 + k];
-          dqa[1][k] = x[7 + k];
-        }
-        ++svd_count;
+        T f;
+        minnorm_combine(z[arm][0], pv[arm][0], z[1 - arm][0], pv[1 - arm][0], sa[arm], f);
+        for (int k = 0; k < 6; ++k) dqa[arm][k] = z[arm][1 + k] + f * pv[arm][1 + k];
       }
       if (sa[0] != sa[1]) std::abort();  // both lanes must carry the same chest step
       ++lq_count;
+      if (pv[0][0] < T(Prec<T>::kRcond) || pv[1][0] < T(Prec<T>::kRcond)) ++svd_count;  // an arm pins s
     }
     ++it;
     for (int arm = 0; arm < 2; ++arm) {

@@ -68,6 +68,17 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
 }
 
 
+#ifdef IKG_SING_COUNT
+extern "C" int ikg_debug_sing(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sing), sizeof(g_sing)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[4] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_sing), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
 // Multi-start best-seed reduction: one wave per target reduces the S seed
 // results the pair kernel wrote for it (key = worse hand error, converged
 // seeds first, ties to the lower seed index) with DPP/permute wave reductions,

@@ -70,19 +70,13 @@ inline void build_kmodel(const ikg_model_desc& d, KModel<T>& k) {
   // arm solve's cancellation (u - s v with |u|, |v| ~ 1/tau) would cost more
   // than ~1e-12 (fp64) / 1e-5 (fp32) of the step, so the pair takes the
   // 6 x 7 LQ form instead
+  k.sing_beta = (T)(sizeof(T) == 8 ? IKG_SING_BETA64 : IKG_SING_BETA32);
   k.sing_tau = (T)(sizeof(T) == 8 ? IKG_SING_TAU64 : IKG_SING_TAU32);
-  // test knob: IKG_SING_TAU=<tau> when the tables are built (1e30: every
-  // update takes the LQ form; 0: never)
+  // test knobs, read when the tables are built: IKG_SING_BETA=0 (with
+  // IKG_SING_TAU=1e30 for the generic path) sends every update through the
+  // LQ form
+  if (const char* e = std::getenv("IKG_SING_BETA")) k.sing_beta = (T)std::atof(e);
   if (const char* e = std::getenv("IKG_SING_TAU")) k.sing_tau = (T)std::atof(e);
-  for (int a = 0; a < 2; ++a) {
-    double L = 0.0;
-    for (int j = 1; j < 5; ++j) {
-      const double* t = d.placement[d.arm_q[a][j]] + 9;
-      L += std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
-    }
-    k.sing_wx[a] = (T)((double)k.sing_tau * L);
-    k.sing_det2[a] = (T)((double)k.sing_tau * L * L);
-  }
   bool used[IKG_MAX_NQ] = {};
   used[r] = true;
   for (int a = 0; a < 2; ++a)

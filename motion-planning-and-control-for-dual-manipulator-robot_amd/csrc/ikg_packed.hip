@@ -21,7 +21,7 @@ namespace ikg {
 //
 // WPS (waves per SIMD cap, 0 = none): the kernel claims AGPRs it never uses (an
 // empty asm clobber) so that the hardware fits at most WPS of its waves on a
-// SIMD -- all 256 for WPS = 1; 16 for WPS = 2 (158 VGPRs + 16 > 512 / 3).  A
+// SIMD -- all 256 AGPRs for WPS = 1; VGPR 171 for WPS = 2 (> 512 / 3).  A
 // launch of at most WPS waves per SIMD then cannot be dispatched with more
 // waves sharing a SIMD while another idles, which the dispatcher does after
 // some kernels (after the collision continuation, 19-46 of 1,024 SIMDs held two
@@ -39,7 +39,10 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               int32_t* __restrict__ iters_out,
                                                               float* __restrict__ err_out) {
   if constexpr (WPS == 1) asm volatile("" ::: "a255");
-  if constexpr (WPS == 2) asm volatile("" ::: "a15");
+  // v171: at least 172 VGPRs, so 2 waves fit and 3 do not; an AGPR claim
+  // instead makes the allocator split the 2-wave budget 128 VGPR / 128 AGPR
+  // and spill the loop (with the guarded step's cold branch in the kernel)
+  if constexpr (WPS == 2) asm volatile("" ::: "v171");
   const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (p >= B) return;
   const int64_t tgt = S > 1 ? p / S : p;

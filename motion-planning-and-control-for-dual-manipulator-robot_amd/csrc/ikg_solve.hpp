@@ -139,7 +139,7 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     ArmState<T> st;
     x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, tkp, resync);
     if constexpr (!DAMPED) {
-      pinv_step_cf<T, SP>(st, arm, T(m->sing_tau), dq, s);
+      pinv_step_cf<T, SP>(st, arm, T(m->sing_tau), T(m->sing_beta), dq, s);
     } else {
       T A[6][8], ze[6], zc[6];
       arm_system(st, A);

@@ -36,3 +36,71 @@ def solve(targets, q0, max_iters=1000, eps=1e-3, dt=1e-2, threads=0):
     load().ikg_oracle_solve(tg.ctypes.data, q.ctypes.data, stride, B, max_iters, eps, dt, q_out.ctypes.data,
                             conv.ctypes.data, iters.ctypes.data, err.ctypes.data, threads)
     return q_out, conv.astype(bool), iters, err
+
+
+def has_collision():
+    """The C restatement of the collision term (ikg_oracle_solve_collision) is built in."""
+    return hasattr(load(), "ikg_oracle_solve_collision")
+
+
+def _scene_arrays(scene):
+    """collision_oracle scene (dict from load_scene / prepare) -> the C arrays."""
+    gs = scene["geoms"]
+    a = dict(
+        kind=np.ascontiguousarray([g["kind"] for g in gs], dtype=np.int32),
+        joint=np.ascontiguousarray([g["joint"] for g in gs], dtype=np.int32),
+        R=np.ascontiguousarray([np.asarray(g["R"], dtype=np.float64).reshape(9) for g in gs]),
+        t=np.ascontiguousarray([np.asarray(g["t"], dtype=np.float64).reshape(3) for g in gs]),
+        dims=np.ascontiguousarray([np.asarray(g["dims"], dtype=np.float64).reshape(3) for g in gs]),
+        target=np.ascontiguousarray([bool(g["target"]) for g in gs], dtype=np.uint8),
+        pairs=np.ascontiguousarray(np.asarray(scene["pairs"], dtype=np.int32).reshape(-1, 2)),
+    )
+    return a
+
+
+def _scene_args(a):
+    return [len(a["kind"]), a["kind"].ctypes.data, a["joint"].ctypes.data, a["R"].ctypes.data, a["t"].ctypes.data,
+            a["dims"].ctypes.data, a["target"].ctypes.data, len(a["pairs"]), a["pairs"].ctypes.data]
+
+
+_SCENE_T = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]
+
+
+def solve_collision(scene, targets, q0, max_iters=1000, eps=1e-3, dt=1e-2, threads=0):
+    """computeqgrasppose WITH the collision term (inverse_geometry.py:70, :97-98),
+    restating collision_oracle.computeqgrasppose in C."""
+    lib = load()
+    f = lib.ikg_oracle_solve_collision
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_double, C.c_double] + _SCENE_T + \
+        [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    f.restype = C.c_int
+    a = _scene_arrays(scene)
+    tg = np.ascontiguousarray(targets, dtype=np.float64).reshape(-1, 12)
+    B = tg.shape[0]
+    q = np.ascontiguousarray(q0, dtype=np.float64)
+    stride = 0 if q.ndim == 1 else 15
+    q_out = np.empty((B, 15))
+    conv = np.empty(B, dtype=np.uint8)
+    iters = np.empty(B, dtype=np.int32)
+    err = np.empty((B, 2))
+    rc = f(tg.ctypes.data, q.ctypes.data, stride, B, max_iters, eps, dt, *_scene_args(a), q_out.ctypes.data,
+           conv.ctypes.data, iters.ctypes.data, err.ctypes.data, threads)
+    if rc != 0:
+        raise ValueError("scene has more than 64 geometries")
+    return q_out, conv.astype(bool), iters, err
+
+
+def collision(scene, q, targets):
+    """tools.collision (tools.py:25-35) per row: q [B,15], targets [B,12] (R row-major, t)."""
+    lib = load()
+    f = lib.ikg_oracle_collision
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int64] + _SCENE_T + [C.c_void_p]
+    f.restype = C.c_int
+    a = _scene_arrays(scene)
+    qq = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, 15)
+    tg = np.ascontiguousarray(targets, dtype=np.float64).reshape(-1, 12)
+    assert len(qq) == len(tg)
+    out = np.empty(len(qq), dtype=np.uint8)
+    if f(qq.ctypes.data, tg.ctypes.data, len(qq), *_scene_args(a), out.ctypes.data) != 0:
+        raise ValueError("scene has more than 64 geometries")
+    return out.astype(bool)

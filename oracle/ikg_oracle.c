@@ -12,6 +12,8 @@
  *   pinv(J) @ e (:83)                -> J^T (J J^T)^-1 e by a 12x12 Cholesky
  *                                       (equal to the pseudo-inverse for full-row-rank J)
  *   integrate + clip (:86, :89)      -> q + dq*DT, clipped to the URDF limits
+ * With a collision scene (ikg_oracle_solve_collision) the stop test also
+ * requires collision(q) to be false (:70), restating oracle/collision_oracle.py.
  * The model tables are transcribed from NextageaOpen.urdf:580-730 and
  * cube_small.urdf:34-47 (same numbers as oracle/ik_oracle.py).
  * Parity: pinned to KAT-1/KAT-2 by tests/test_oracle_c.py.
@@ -231,8 +233,257 @@ static void hand_errors(const double* q, const se3 tgt[2], double e[12], double 
   }
 }
 
+/* ---------------------------------------------------------------- collision term
+ * Restates oracle/collision_oracle.py (itself the hpp-fcl semantics the
+ * reference's tools.collision relies on, tools.py:25-35): a pair collides when
+ * the two convex shapes intersect.  Sphere/sphere and sphere/box exact,
+ * box/box by the 15-axis separating-axis test, every pair with a cylinder by
+ * boolean GJK on support functions.  The scene (geometries in their parent
+ * joint frames, active pairs; the target geometry is placed at the cube
+ * target) comes from the caller (tests/golden/collision_scene.json). */
+enum { K_SPHERE = 0, K_BOX = 1, K_CYL = 2, K_MESHBOX = 3 };
+
+typedef struct {
+  int n_geoms, n_pairs;
+  const int32_t* kind;
+  const int32_t* joint;  /* q index of the parent joint, -1 = world */
+  const double* R;       /* [g][9] placement in the parent joint frame (world if joint < 0) */
+  const double* t;       /* [g][3] */
+  const double* dims;    /* [g][3] */
+  const uint8_t* target; /* placed at the solve's cube target */
+  const int32_t* pairs;  /* [k][2] */
+} col_scene;
+
+typedef struct {
+  int kind;
+  double R[3][3], t[3], d[3];
+} shape;
+
+static double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static void cross3(const double* a, const double* b, double* c) {
+  double r0 = a[1] * b[2] - a[2] * b[1], r1 = a[2] * b[0] - a[0] * b[2], r2 = a[0] * b[1] - a[1] * b[0];
+  c[0] = r0, c[1] = r1, c[2] = r2;
+}
+
+static void support(const shape* g, const double* d, double* out) {
+  if (g->kind == K_SPHERE) {
+    double n = sqrt(dot3(d, d));
+    for (int i = 0; i < 3; ++i) out[i] = g->t[i] + (n > 0 ? g->d[0] * d[i] / n : 0.0);
+    return;
+  }
+  double dl[3], loc[3];
+  for (int i = 0; i < 3; ++i) dl[i] = g->R[0][i] * d[0] + g->R[1][i] * d[1] + g->R[2][i] * d[2];
+  if (g->kind == K_BOX || g->kind == K_MESHBOX) {
+    for (int i = 0; i < 3; ++i) loc[i] = (dl[i] >= 0 ? 1.0 : -1.0) * g->d[i];
+  } else {
+    double rad = hypot(dl[0], dl[1]);
+    loc[0] = rad > 0 ? g->d[0] * dl[0] / rad : 0.0;
+    loc[1] = rad > 0 ? g->d[0] * dl[1] / rad : 0.0;
+    loc[2] = dl[2] >= 0 ? g->d[1] : -g->d[1];
+  }
+  for (int i = 0; i < 3; ++i) out[i] = g->t[i] + g->R[i][0] * loc[0] + g->R[i][1] * loc[1] + g->R[i][2] * loc[2];
+}
+
+static void mink(const shape* a, const shape* b, const double* d, double* out) {
+  double pa[3], pb[3], nd[3] = {-d[0], -d[1], -d[2]};
+  support(a, d, pa);
+  support(b, nd, pb);
+  for (int i = 0; i < 3; ++i) out[i] = pa[i] - pb[i];
+}
+
+/* the simplex step of collision_oracle._do_simplex: s[0..n-1] oldest first,
+ * s[n-1] newest; returns 1 when the origin is enclosed */
+static int do_simplex(double s[4][3], int* n, double* d) {
+  double* a = s[*n - 1];
+  double ao[3] = {-a[0], -a[1], -a[2]};
+  if (*n == 2) {
+    double ab[3], t[3];
+    for (int i = 0; i < 3; ++i) ab[i] = s[0][i] - a[i];
+    if (dot3(ab, ao) > 0) {
+      cross3(ab, ao, t);
+      if (sqrt(dot3(t, t)) > 1e-15) {
+        cross3(t, ab, d);
+      } else { /* _perp(ab) */
+        double e[3] = {fabs(ab[0]) < 0.9 ? 1.0 : 0.0, fabs(ab[0]) < 0.9 ? 0.0 : 1.0, 0.0};
+        cross3(ab, e, d);
+      }
+      return 0; /* simplex [b, a] unchanged */
+    }
+    memcpy(s[0], a, sizeof(s[0]));
+    *n = 1;
+    memcpy(d, ao, sizeof(ao));
+    return 0;
+  }
+  if (*n == 3) {
+    double c[3], b[3], ab[3], ac[3], abc[3], t[3];
+    memcpy(c, s[0], sizeof(c));
+    memcpy(b, s[1], sizeof(b));
+    for (int i = 0; i < 3; ++i) ab[i] = b[i] - a[i], ac[i] = c[i] - a[i];
+    cross3(ab, ac, abc);
+    cross3(abc, ac, t);
+    if (dot3(t, ao) > 0) {
+      if (dot3(ac, ao) > 0) {
+        double a_[3];
+        memcpy(a_, a, sizeof(a_));
+        memcpy(s[0], c, sizeof(c));
+        memcpy(s[1], a_, sizeof(a_));
+        *n = 2;
+        cross3(ac, ao, t);
+        cross3(t, ac, d);
+        return 0;
+      }
+      double a_[3];
+      memcpy(a_, a, sizeof(a_));
+      memcpy(s[0], b, sizeof(b));
+      memcpy(s[1], a_, sizeof(a_));
+      *n = 2;
+      return do_simplex(s, n, d);
+    }
+    cross3(ab, abc, t);
+    if (dot3(t, ao) > 0) {
+      double a_[3];
+      memcpy(a_, a, sizeof(a_));
+      memcpy(s[0], b, sizeof(b));
+      memcpy(s[1], a_, sizeof(a_));
+      *n = 2;
+      return do_simplex(s, n, d);
+    }
+    if (dot3(abc, ao) > 0) { /* [c, b, a] */
+      memcpy(d, abc, sizeof(abc));
+      return 0;
+    }
+    /* [b, c, a] */
+    memcpy(s[0], b, sizeof(b));
+    memcpy(s[1], c, sizeof(c));
+    for (int i = 0; i < 3; ++i) d[i] = -abc[i];
+    return 0;
+  }
+  double dd[3], c[3], b[3], ab[3], ac[3], ad[3], abc[3], acd[3], adb[3];
+  memcpy(dd, s[0], sizeof(dd));
+  memcpy(c, s[1], sizeof(c));
+  memcpy(b, s[2], sizeof(b));
+  for (int i = 0; i < 3; ++i) ab[i] = b[i] - a[i], ac[i] = c[i] - a[i], ad[i] = dd[i] - a[i];
+  cross3(ab, ac, abc);
+  cross3(ac, ad, acd);
+  cross3(ad, ab, adb);
+  double a_[3];
+  memcpy(a_, a, sizeof(a_));
+  if (dot3(abc, ao) > 0) {
+    memcpy(s[0], c, sizeof(c)), memcpy(s[1], b, sizeof(b)), memcpy(s[2], a_, sizeof(a_));
+    *n = 3;
+    return do_simplex(s, n, d);
+  }
+  if (dot3(acd, ao) > 0) {
+    memcpy(s[0], dd, sizeof(dd)), memcpy(s[1], c, sizeof(c)), memcpy(s[2], a_, sizeof(a_));
+    *n = 3;
+    return do_simplex(s, n, d);
+  }
+  if (dot3(adb, ao) > 0) {
+    memcpy(s[0], b, sizeof(b)), memcpy(s[1], dd, sizeof(dd)), memcpy(s[2], a_, sizeof(a_));
+    *n = 3;
+    return do_simplex(s, n, d);
+  }
+  return 1;
+}
+
+static int gjk_intersect(const shape* a, const shape* b) {
+  double s[4][3], d[3];
+  for (int i = 0; i < 3; ++i) d[i] = a->t[i] - b->t[i];
+  if (!(dot3(d, d) > 0)) d[0] = 1.0, d[1] = d[2] = 0.0;
+  mink(a, b, d, s[0]);
+  int n = 1;
+  for (int i = 0; i < 3; ++i) d[i] = -s[0][i];
+  for (int it = 0; it < 64; ++it) {
+    if (dot3(d, d) < 1e-30) return 1;
+    double p[3];
+    mink(a, b, d, p);
+    if (dot3(p, d) < 0) return 0;
+    memcpy(s[n++], p, sizeof(p));
+    if (do_simplex(s, &n, d)) return 1;
+  }
+  return 1;
+}
+
+static int box_box(const shape* a, const shape* b) {
+  double ax[15][3];
+  int k = 0;
+  for (int i = 0; i < 3; ++i, ++k)
+    for (int r = 0; r < 3; ++r) ax[k][r] = a->R[r][i];
+  for (int i = 0; i < 3; ++i, ++k)
+    for (int r = 0; r < 3; ++r) ax[k][r] = b->R[r][i];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j, ++k) {
+      double ci[3] = {a->R[0][i], a->R[1][i], a->R[2][i]}, cj[3] = {b->R[0][j], b->R[1][j], b->R[2][j]};
+      cross3(ci, cj, ax[k]);
+    }
+  double d[3] = {b->t[0] - a->t[0], b->t[1] - a->t[1], b->t[2] - a->t[2]};
+  for (k = 0; k < 15; ++k) {
+    double n = sqrt(dot3(ax[k], ax[k]));
+    if (n < 1e-12) continue;
+    double u[3] = {ax[k][0] / n, ax[k][1] / n, ax[k][2] / n};
+    double r1 = 0, r2 = 0;
+    for (int i = 0; i < 3; ++i) {
+      double ci[3] = {a->R[0][i], a->R[1][i], a->R[2][i]}, cj[3] = {b->R[0][i], b->R[1][i], b->R[2][i]};
+      r1 += a->d[i] * fabs(dot3(ci, u));
+      r2 += b->d[i] * fabs(dot3(cj, u));
+    }
+    if (fabs(dot3(d, u)) > r1 + r2) return 0;
+  }
+  return 1;
+}
+
+static int collide(const shape* a, const shape* b) {
+  int ka = a->kind, kb = b->kind;
+  int bxa = ka == K_BOX || ka == K_MESHBOX, bxb = kb == K_BOX || kb == K_MESHBOX;
+  if (ka == K_SPHERE && kb == K_SPHERE) {
+    double d[3] = {a->t[0] - b->t[0], a->t[1] - b->t[1], a->t[2] - b->t[2]};
+    return sqrt(dot3(d, d)) < a->d[0] + b->d[0];
+  }
+  if ((ka == K_SPHERE && bxb) || (kb == K_SPHERE && bxa)) {
+    const shape* sp = ka == K_SPHERE ? a : b;
+    const shape* bx = ka == K_SPHERE ? b : a;
+    double w[3] = {sp->t[0] - bx->t[0], sp->t[1] - bx->t[1], sp->t[2] - bx->t[2]}, p[3], e2 = 0;
+    for (int i = 0; i < 3; ++i) p[i] = bx->R[0][i] * w[0] + bx->R[1][i] * w[1] + bx->R[2][i] * w[2];
+    for (int i = 0; i < 3; ++i) {
+      double c = p[i] < -bx->d[i] ? -bx->d[i] : (p[i] > bx->d[i] ? bx->d[i] : p[i]);
+      e2 += (p[i] - c) * (p[i] - c);
+    }
+    return sqrt(e2) < sp->d[0];
+  }
+  if (bxa && bxb) return box_box(a, b);
+  return gjk_intersect(a, b);
+}
+
+/* tools.collision (tools.py:25-35) at q with the cube target `cube` */
+static int collides(const col_scene* sc, const double* q, const se3* cube) {
+  se3 oMi[NQ];
+  fk(q, oMi);
+  shape g[64];
+  if (sc->n_geoms > 64) return -1;
+  for (int k = 0; k < sc->n_geoms; ++k) {
+    se3 loc, w;
+    for (int i = 0; i < 3; ++i) {
+      for (int j = 0; j < 3; ++j) loc.R[i][j] = sc->R[9 * k + 3 * i + j];
+      loc.t[i] = sc->t[3 * k + i];
+    }
+    if (sc->target[k])
+      w = *cube;
+    else if (sc->joint[k] < 0)
+      w = loc;
+    else
+      mul(&oMi[sc->joint[k]], &loc, &w);
+    g[k].kind = sc->kind[k];
+    memcpy(g[k].R, w.R, sizeof(w.R));
+    memcpy(g[k].t, w.t, sizeof(w.t));
+    for (int i = 0; i < 3; ++i) g[k].d[i] = sc->dims[3 * k + i];
+  }
+  for (int p = 0; p < sc->n_pairs; ++p)
+    if (collide(&g[sc->pairs[2 * p]], &g[sc->pairs[2 * p + 1]])) return 1;
+  return 0;
+}
+
 static void solve_one(const double* target, const double* q0, int max_iters, double eps, double dt, double* q_out,
-                      uint8_t* conv, int32_t* iters, double* err) {
+                      uint8_t* conv, int32_t* iters, double* err, const col_scene* sc) {
   se3 cube, hook, tgt[2];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) cube.R[i][j] = target[3 * i + j];
@@ -253,7 +504,8 @@ static void solve_one(const double* target, const double* q0, int max_iters, dou
   for (;;) {
     hand_errors(q, tgt, e, n);
     if (it >= max_iters) break;
-    if (n[0] < eps && n[1] < eps) {
+    /* :70 -- errors pass and (with a scene) not collision(q) */
+    if (n[0] < eps && n[1] < eps && !(sc && collides(sc, q, &cube))) {
       ok = 1;
       break;
     }
@@ -285,7 +537,43 @@ int ikg_oracle_solve(const double* targets, const double* q0, int64_t q0_stride,
 #endif
   for (int64_t i = 0; i < B; ++i)
     solve_one(targets + 12 * i, q0 + q0_stride * i, max_iters, eps, dt, q_out + NQ * i, conv + i, iters + i,
-              err + 2 * i);
+              err + 2 * i, NULL);
+  return 0;
+}
+
+/* The loop WITH the collision term (inverse_geometry.py:70, :97-98): the
+ * scene arrays as col_scene documents them. */
+int ikg_oracle_solve_collision(const double* targets, const double* q0, int64_t q0_stride, int64_t B, int max_iters,
+                               double eps, double dt, int n_geoms, const int32_t* kind, const int32_t* joint,
+                               const double* R, const double* t, const double* dims, const uint8_t* target,
+                               int n_pairs, const int32_t* pairs, double* q_out, uint8_t* conv, int32_t* iters,
+                               double* err, int nthreads) {
+  if (n_geoms > 64) return -1;
+  col_scene sc = {n_geoms, n_pairs, kind, joint, R, t, dims, target, pairs};
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t i = 0; i < B; ++i)
+    solve_one(targets + 12 * i, q0 + q0_stride * i, max_iters, eps, dt, q_out + NQ * i, conv + i, iters + i,
+              err + 2 * i, &sc);
+  return 0;
+}
+
+/* tools.collision alone, for the tests: out[i] = collision(q_i, target_i) */
+int ikg_oracle_collision(const double* q, const double* targets, int64_t B, int n_geoms, const int32_t* kind,
+                         const int32_t* joint, const double* R, const double* t, const double* dims,
+                         const uint8_t* target, int n_pairs, const int32_t* pairs, uint8_t* out) {
+  if (n_geoms > 64) return -1;
+  col_scene sc = {n_geoms, n_pairs, kind, joint, R, t, dims, target, pairs};
+  for (int64_t i = 0; i < B; ++i) {
+    se3 cube;
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c) cube.R[r][c] = targets[12 * i + 3 * r + c];
+      cube.t[r] = targets[12 * i + 9 + r];
+    }
+    out[i] = (uint8_t)collides(&sc, q + NQ * i, &cube);
+  }
   return 0;
 }
 

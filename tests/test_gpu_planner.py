@@ -108,7 +108,11 @@ def test_project_paths_batch_equals_dropin(robot_cube, pc):
         one, _ = project_path(robot, cube, pc[f"{k}_start_q"], SE3(np.eye(3), pc[f"{k}_start_t"]),
                               SE3(np.eye(3), pc[f"{k}_goal_t"]))
         assert len(rp) == len(one)
-        assert np.array_equal(np.array(rp), np.array(one))
+        # the drop-in's warm start is a broadcast q0, whose post-convergence
+        # records come from the batch kernel (trig state carried on); the
+        # batched chains pass one q0 row each, recorded by the trajectory
+        # kernel (trig resynced per window): the same iterates to rounding
+        assert np.abs(np.array(rp) - np.array(one)).max() <= 1e-12
 
 
 def test_planner_queries_reject_bad_arguments(robot_cube):

@@ -6,7 +6,7 @@ on all 48 cases, q within max(1e-9, 2e-19 cond(J)); identical to the numpy
 oracle where cond(J) < 1e6, q within 1e-9.  fp32 (pair and packed layouts):
 where cond(J) < 1e6, flags identical, updates within +-2 and end-effector
 error <= 1e-4 per hand for converged solves.  The guard's LQ branch is also
-run on every update (IKG_SING_TAU=1e30) against the ordinary fixtures, in the
+run on every update (IKG_SING_BETA=0) against the ordinary fixtures, in the
 batch, multi-start and collision paths."""
 import os
 
@@ -58,21 +58,21 @@ def test_singular_seeds_fp32(solver, sing, variant):
 
 @pytest.fixture(scope="module")
 def lq_solver():
-    """A solver whose tables were built with IKG_SING_TAU=1e30: every update
+    """A solver whose tables were built with IKG_SING_BETA=0: every update
     takes the guard's LQ branch."""
     from ikgrasp.collision import load_nextage_scene
     from ikgrasp.solver import IKSolver
-    old = os.environ.get("IKG_SING_TAU")
-    os.environ["IKG_SING_TAU"] = "1e30"
+    old = os.environ.get("IKG_SING_BETA")
+    os.environ["IKG_SING_BETA"] = "0"
     try:
         s = IKSolver(device=0, scene=load_nextage_scene())
         s.solve(np.zeros((1, 12)) + np.concatenate([np.eye(3).ravel(), [0.4, 0.1, 0.93]]), np.zeros(15))
         s.solve(np.zeros((1, 12)) + np.concatenate([np.eye(3).ravel(), [0.4, 0.1, 0.93]]), np.zeros(15), dtype="f32")
     finally:
         if old is None:
-            del os.environ["IKG_SING_TAU"]
+            del os.environ["IKG_SING_BETA"]
         else:
-            os.environ["IKG_SING_TAU"] = old
+            os.environ["IKG_SING_BETA"] = old
     yield s
     s.close()
 

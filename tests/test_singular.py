@@ -119,9 +119,9 @@ def test_emulated_kernel_fp32_at_singularities(emu, sing):
 
 
 def test_lq_form_everywhere_reproduces_the_fixtures(emu, oracle_cases, monkeypatch):
-    """IKG_SING_TAU=1e30 sends every update through the LQ form (the guard's
+    """IKG_SING_BETA=0 sends every update through the LQ form (the guard's
     branch): the 96 oracle fixtures come out as with the closed form."""
-    monkeypatch.setenv("IKG_SING_TAU", "1e30")
+    monkeypatch.setenv("IKG_SING_BETA", "0")
     c = oracle_cases
     emu.lib.ikg_emu_lq_count(1)
     q, conv, it = emu(c["targets"], c["q0"])
