@@ -1,0 +1,114 @@
+"""BASELINE.json configs at their stated sizes against the oracle (run on an MI355X).
+
+* C3 (65,536 targets, fp32): a seeded sample of 512 targets re-solved by the C
+  oracle (oracle/ikg_oracle.c, fp64, min-norm solve = pinv(J) e for full-rank J,
+  inverse_geometry.py:83); the mismatch counts the gates allow are printed and,
+  with IKG_REPORT_DIR set, written to <dir>/c3_vs_oracle.json.
+* C5 (multi-start, per-GPU share: 256 seeds x 512 targets), fp64 and both fp32
+  layouts: the best seed equals the argmin over the expanded (target, seed)
+  batch solve, and 64 targets re-solved by the oracle from their winning seed
+  agree (fp64: identical flags and update counts, q within 1e-9; fp32:
+  end-effector error <= 1e-4, counts within +-2).  The reference's analogue is
+  the resample-until-success loop of path.py:39-67.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import helpers
+from oracle import c_oracle
+from oracle import ik_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def _report(name, d):
+    print(f"{name}: {json.dumps(d)}")
+    out = os.environ.get("IKG_REPORT_DIR")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, f"{name}.json"), "w") as f:
+            json.dump(d, f, indent=1)
+
+
+def _ee_err(solver, qa, qb):
+    """Per-hand |log6(Ma^-1 Mb)| between two q batches (both via the fp64 FK kernel)."""
+    ha = solver.fk(np.asarray(qa, dtype=np.float64))
+    hb = solver.fk(np.asarray(qb, dtype=np.float64))
+    e = [helpers.se3_err(ha[:, h, :9].reshape(-1, 3, 3), ha[:, h, 9:], hb[:, h, :9].reshape(-1, 3, 3), hb[:, h, 9:])
+         for h in range(2)]
+    return np.maximum(e[0], e[1])
+
+
+def test_c3_sample_against_oracle(solver):
+    from ikgrasp.workload import uniform_targets
+    B = 65536
+    tg = uniform_targets(B, seed=1)
+    s32 = solver.solve(tg, np.zeros(15), dtype="f32")  # AUTO: the packed layout at this size
+    idx = np.sort(np.random.default_rng(31).choice(B, 512, replace=False))
+    q, conv, iters, _ = c_oracle.solve(tg[idx], np.zeros(15))
+    g_conv, g_it = s32.converged[idx], s32.iters[idx].astype(int)
+    both = conv & g_conv
+    flag_mis = int((conv != g_conv).sum())
+    it_off = np.abs(g_it[both] - iters[both])
+    ee = _ee_err(solver, q[both], s32.q[idx][both])
+    rep = dict(sample=512, oracle_converged=int(conv.sum()), gpu_converged=int(g_conv.sum()),
+               flag_mismatches=flag_mis, iters_outside_pm2=int((it_off > 2).sum()),
+               iters_max_abs_diff=int(it_off.max()) if it_off.size else 0,
+               ee_err_max=float(ee.max()) if ee.size else 0.0)
+    _report("c3_vs_oracle", rep)
+    # gates: SURVEY §8d C3 (EE <= 1e-4, counts +-2); a flag may flip only where the
+    # fp32 and fp64 error norms straddle eps within fp32 rounding
+    assert flag_mis <= 2
+    assert rep["iters_outside_pm2"] <= 2
+    assert rep["ee_err_max"] <= 1e-4
+
+
+@pytest.mark.parametrize("dtype,variant", [("f64", 0), ("f32", 1), ("f32", 2)])  # AUTO, PAIR, PACKED
+def test_c5_share_multistart(solver, dtype, variant):
+    from ikgrasp.workload import random_seeds, uniform_targets
+    T, S = 512, 256
+    tg = uniform_targets(T, seed=41)
+    seeds = random_seeds(solver.model, S, seed=42)
+    seeds[0] = 0.0  # robot.q0, the reference's seed
+    ms = solver.solve_multistart(tg, seeds, dtype=dtype, variant=variant)
+    full = solver.solve(np.repeat(tg, S, axis=0), np.tile(seeds, (T, 1)), dtype=dtype, variant=variant)
+    conv = full.converged.reshape(T, S)
+    worst = full.err.max(axis=1).reshape(T, S).astype(np.float64)
+    key = np.where(conv, worst, 1e30 + worst)
+    best = key.argmin(axis=1)
+    assert np.array_equal(ms.best_seed, best)
+    k = np.arange(T) * S + best
+    assert np.array_equal(ms.q, full.q[k])
+    assert np.array_equal(ms.converged, full.converged[k]) and np.array_equal(ms.iters, full.iters[k])
+    # the uniform sampler draws some unreachable targets: 256 seeds solve ~64%
+    # of them, against ~40% for the single seed q0 (C2)
+    assert ms.converged.mean() > 0.5
+
+    # 64 targets against the oracle from their winning seed
+    sel = np.random.default_rng(43).choice(T, 64, replace=False)
+    q, oc, oi, _ = c_oracle.solve(tg[sel], seeds[best[sel]])
+    g_conv, g_it = ms.converged[sel], ms.iters[sel].astype(int)
+    rep = dict(dtype=dtype, variant=variant, T=T, S=S, best_converged=int(ms.converged.sum()),
+               sample=64, flag_mismatches=int((oc != g_conv).sum()))
+    both = oc & g_conv
+    if dtype == "f64":
+        assert np.array_equal(oc, g_conv) and np.array_equal(oi, g_it)
+        dq = np.abs(q[both] - ms.q[sel][both]).max()
+        rep["q_max_abs_diff"] = float(dq)
+        assert dq <= 1e-9
+    else:
+        it_off = np.abs(g_it[both] - oi[both])
+        ee = _ee_err(solver, q[both], ms.q[sel][both])
+        rep.update(iters_outside_pm2=int((it_off > 2).sum()), ee_err_max=float(ee.max()))
+        assert rep["flag_mismatches"] <= 1 and rep["iters_outside_pm2"] <= 1 and rep["ee_err_max"] <= 1e-4
+    # a few through the pinv restatement itself (np.linalg.pinv, inverse_geometry.py:83)
+    for j in sel[:4]:
+        qp, okp, itp, _ = o.computeqgrasppose(seeds[best[j]].copy(), tg[j, :9].reshape(3, 3), tg[j, 9:])
+        if dtype == "f64":
+            assert okp == ms.converged[j] and itp == ms.iters[j] and np.abs(qp - ms.q[j]).max() <= 1e-9
+        elif okp and ms.converged[j]:
+            assert abs(itp - int(ms.iters[j])) <= 2
+    _report(f"c5_share_{dtype}_v{variant}", rep)

@@ -1,12 +1,16 @@
-"""Executed FP operations per problem-iteration of the batch kernel, from
+"""Executed FP operations per problem-iteration of a batch kernel, from
 rocprofv3 --pmc instruction counters (tools/pmc_flops.sh), for bench.py's
-roofline.executed_frac.
+roofline.executed.
 
-A wave-level VALU instruction runs on the wave's 64 lanes; the pair layout
-puts 2 lanes on a problem, so one problem-iteration issues (per lane)
-2*FMA + MUL + ADD + TRANS FP operations on each of its 2 lanes.  Lanes of
-problems that have already stopped are masked off but still occupy the
-issue slot, so the counts are divided by the wave-iterations the launch
+Pair layout (ikg_pair_batch_kernel): 2 lanes per problem, 32 problems per
+wave; one problem-iteration issues (per lane) 2*FMA + MUL + ADD + TRANS FP
+operations on each of its 2 lanes.  Packed layout (ikg_packed_batch_kernel,
+fp32): one lane per problem, 64 problems per wave, both arms in 2-vectors;
+SQ_INSTS_VALU_*_F32 count a v_pk_* instruction once, so its second half is
+counted from the packed-instruction counter (SQ_INSTS_VALU_PK_* is not
+collected on gfx950 here: the figure is a lower bound and says so).
+Lanes of problems that have already stopped are masked off but still occupy
+the issue slot, so the counts are divided by the wave-iterations the launch
 actually ran: sum over waves of (max updates in the wave + 1 evaluations).
 
 usage: python tools/pmc_flops.py gpurun_out/flops/<dtype>_b<B> B dtype tag"""
@@ -19,19 +23,23 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNELS = {"ikg_pair_batch_kernel": ("pair", 32, 2), "ikg_packed_batch_kernel": ("packed", 64, 1)}
 
 
 def main(d, B, dtype, tag):
     sfx = "F64" if dtype == "f64" else "F32"
-    per = {}
+    per, kname = {}, None
     for r in csv.DictReader(open(os.path.join(d, "ops", "run_counter_collection.csv"))):
-        if "ikg_pair_batch_kernel" not in r["Kernel_Name"]:
+        k = next((k for k in KERNELS if k in r["Kernel_Name"]), None)
+        if k is None:
             continue
+        kname = k
         per.setdefault(r["Dispatch_Id"], {}).setdefault(r["Counter_Name"], 0.0)
         per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+    short, ppw, lanes = KERNELS[kname]
     it = np.load(os.path.join(d, "iters.npy"))
-    ppw = 32
-    waves = it.reshape(-1, ppw) if len(it) % ppw == 0 else None
+    pad = (-len(it)) % ppw
+    waves = np.concatenate([it, np.full(pad, -1)]).reshape(-1, ppw)
     wave_iters = float((waves.max(axis=1) + 1).sum())
     ops = []
     for c in per.values():
@@ -39,15 +47,19 @@ def main(d, B, dtype, tag):
             c[f"SQ_INSTS_VALU_TRANS_{sfx}"]
         ops.append(fp / wave_iters)
     lane = statistics.median(ops)
-    out = {"kernel": "ikg_pair_batch_kernel", "dtype": dtype, "batch": B, "round": tag,
-           "fp_ops_per_lane_iter": lane, "fp_ops_per_problem_iter": 2 * lane, "wave_iterations": wave_iters,
+    out = {"kernel": kname, "dtype": dtype, "batch": B, "round": tag, "problems_per_wave": ppw,
+           "fp_ops_per_lane_iter": lane, "fp_ops_per_problem_iter": lanes * lane, "wave_iterations": wave_iters,
            "dispatches": len(ops),
-           "note": "rocprofv3 SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS} (FMA = 2 ops) per wave-iteration, x 2 lanes/problem"}
-    path = os.path.join(ROOT, "profiles", f"flops_{dtype}_b{B}.json")
+           "note": f"rocprofv3 SQ_INSTS_VALU_{{FMA,MUL,ADD,TRANS}}_{sfx} (FMA = 2 ops) per wave-iteration, "
+                   f"x {lanes} lane(s)/problem" +
+                   ("; v_pk_* instructions counted once (lower bound: each carries both arms)"
+                    if short == "packed" else "")}
+    path = os.path.join(ROOT, "profiles", f"flops_{short}_{dtype}.json" if short == "packed" else
+                        f"flops_{dtype}_b{B}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(path, out)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else "r02")
+    main(sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else "r03")

@@ -1,5 +1,6 @@
 """Run one IK configuration `reps` times (for rocprofv3 --pmc passes).
-usage: pmc_probe.py B dtype ppw reps [--save-iters path.npy]"""
+usage: pmc_probe.py B dtype ppw reps [--save-iters path.npy] [--collision]
+--collision: the solve with the collision term (the reference's success)."""
 import os
 import sys
 
@@ -7,11 +8,13 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd"))
+from ikgrasp.collision import load_nextage_scene  # noqa: E402
 from ikgrasp.solver import IKSolver  # noqa: E402
 from ikgrasp.workload import uniform_targets  # noqa: E402
 
 B, dtype, ppw, reps = int(sys.argv[1]), sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
-s = IKSolver()
+col = "--collision" in sys.argv
+s = IKSolver(scene=load_nextage_scene() if col else None)
 dev = torch.device("cuda", 0)
 tdt = torch.float64 if dtype == "f64" else torch.float32
 code = 0 if dtype == "f64" else 1
@@ -23,7 +26,7 @@ it = torch.empty(B, dtype=torch.int32, device=dev)
 er = torch.empty((B, 2), dtype=tdt, device=dev)
 st = torch.cuda.current_stream().cuda_stream
 for _ in range(reps):
-    s.solve_into(tg, q0, qo, cv, it, er, code, st, ppw=ppw)
+    s.solve_into(tg, q0, qo, cv, it, er, code, st, ppw=ppw, check_collision=col)
 torch.cuda.synchronize()
 print("sum iters", int(it.to(torch.int64).sum()), "converged", int(cv.sum()))
 if "--save-iters" in sys.argv:

@@ -22,6 +22,32 @@ def per_dispatch(d, counter):
     return list(vals.values())
 
 
+def per_solve(d, counter, solves):
+    """Collision solves launch several kernels (batch kernel, pre-screen, scan,
+    compaction): every ikg_* dispatch of the run, summed, over the number of
+    identical solves the probe ran."""
+    tot = 0.0
+    for r in csv.DictReader(open(os.path.join(d, "run_counter_collection.csv"))):
+        if r["Kernel_Name"].startswith("ikg_") or " ikg_" in r["Kernel_Name"] or "ikg::" in r["Kernel_Name"]:
+            if r["Counter_Name"] == counter:
+                tot += float(r["Counter_Value"])
+    return tot / solves
+
+
+def main_collision(pmc_dir, dtype, B, tag, solves):
+    fetch = per_solve(os.path.join(pmc_dir, f"fetch_b{B}_{dtype}_col"), "FETCH_SIZE", solves)
+    write = per_solve(os.path.join(pmc_dir, f"write_b{B}_{dtype}_col"), "WRITE_SIZE", solves)
+    out = {"kernel": "collision solve: every ikg_* kernel of one ikg_solve_batch with check_collision",
+           "dtype": dtype, "batch": B, "round": tag, "solves": solves,
+           "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write, "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
+           "note": "2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes; all dispatches of "
+                   "the run over the number of identical solves"}
+    path = os.path.join(ROOT, "profiles", f"pmc_{dtype}_b{B}_col.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print(path, out)
+
+
 def main(pmc_dir, dtype, B, tag):
     fetch = statistics.median(per_dispatch(os.path.join(pmc_dir, f"fetch_b{B}_{dtype}"), "FETCH_SIZE"))
     write = statistics.median(per_dispatch(os.path.join(pmc_dir, f"write_b{B}_{dtype}"), "WRITE_SIZE"))
@@ -39,4 +65,7 @@ def main(pmc_dir, dtype, B, tag):
 
 
 if __name__ == "__main__":
+    if "--collision" in sys.argv:
+        main_collision(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[6]))
+        sys.exit(0)
     main(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else "r01")
