@@ -21,6 +21,11 @@
  *   - All buffers are owned by the caller.  They are device pointers unless
  *     IKG_FLAG_HOST_POINTERS is set, in which case the library stages them
  *     through device scratch and synchronises the stream before returning.
+ *   - Float inputs must be finite.  With IKG_FLAG_HOST_POINTERS the solve
+ *     entry points check targets, q0 and seeds and return IKG_EINVAL for a
+ *     NaN/inf; device-pointer callers own the check (the kernels are built
+ *     with finite-math assumptions, so a non-finite input gives unspecified
+ *     values for that problem's outputs).
  *   - Return 0 on success, a negative IKG_E* code on failure; the message of
  *     the last failure on the calling thread is ikg_last_error().  Nothing
  *     throws or exits across this boundary.

@@ -205,6 +205,18 @@ int check_params(const ikg_params* p) {
   return IKG_OK;
 }
 
+// Host-pointer inputs are checked for finiteness before staging: the device
+// code is compiled with -ffinite-math-only, so a NaN/inf target, q0 row or seed
+// would be undefined there.  Device-pointer callers own that contract
+// (include/ikgrasp.h "Conventions").
+template <typename T>
+int check_finite(const void* p, int64_t n, const char* what) {
+  const T* x = static_cast<const T*>(p);
+  for (int64_t i = 0; i < n; ++i)
+    if (!std::isfinite(x[i])) return fail(IKG_EINVAL, "%s[%lld] is not finite", what, (long long)i);
+  return IKG_OK;
+}
+
 template <typename T>
 ikg::KParams<T> kparams(const ikg_params* p) {
   return ikg::make_kparams<T>(p);
@@ -245,6 +257,9 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   const bool host = flags & IKG_FLAG_HOST_POINTERS;
   if (host) {
     const int64_t q0_rows = q0_stride == 0 ? 1 : B;
+    if ((rc = check_finite<T>(targets, 12 * B, "targets"))) return rc;
+    for (int64_t r = 0; r < q0_rows; ++r)
+      if ((rc = check_finite<T>(static_cast<const T*>(q0) + r * q0_stride, nq, "q0 row"))) return rc;
     a.targets = st.in(targets, sizeof(T) * 12 * B);
     a.q0 = st.in(q0, sizeof(T) * (q0_stride == 0 ? nq : q0_stride * (q0_rows - 1) + nq));
     a.q_out = st.out(sizeof(T) * nq * B);
@@ -337,6 +352,8 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   Staging st(s);
   const bool host = flags & IKG_FLAG_HOST_POINTERS;
   if (host) {
+    if ((rc = check_finite<T>(targets, 12 * T_, "targets")) || (rc = check_finite<T>(seeds, nq * S, "seeds")))
+      return rc;
     a.targets = st.in(targets, sizeof(T) * 12 * T_);
     a.seeds = st.in(seeds, sizeof(T) * nq * S);
     a.q_out = st.out(sizeof(T) * nq * T_);

@@ -68,8 +68,9 @@ def solve_sharded(solver, targets, q0, dtype="f64", dst=0, **kw):
     if q.dim() == 2:
         q = q[lo:hi]
     sol = solver.solve(tg, q, **kw)
+    host = dist.get_backend() == "gloo"  # gloo gathers host tensors (the rehearsal of RCCL's device gather)
     out = {}
     for name, t in (("q", sol.q), ("converged", sol.converged.to(torch.uint8)), ("iters", sol.iters),
                     ("err", sol.err)):
-        out[name] = gather_rows(t, len(targets), dst=dst)
+        out[name] = gather_rows(t.cpu() if host else t, len(targets), dst=dst)
     return out if rank == dst else None

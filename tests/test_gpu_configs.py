@@ -87,28 +87,72 @@ def test_c5_share_multistart(solver, dtype, variant):
     # of them, against ~40% for the single seed q0 (C2)
     assert ms.converged.mean() > 0.5
 
-    # 64 targets against the oracle from their winning seed
+    # 64 targets against the oracles from their winning seed
     sel = np.random.default_rng(43).choice(T, 64, replace=False)
-    q, oc, oi, _ = c_oracle.solve(tg[sel], seeds[best[sel]])
+    rep = dict(dtype=dtype, variant=variant, T=T, S=S, best_converged=int(ms.converged.sum()), sample=64)
     g_conv, g_it = ms.converged[sel], ms.iters[sel].astype(int)
-    rep = dict(dtype=dtype, variant=variant, T=T, S=S, best_converged=int(ms.converged.sum()),
-               sample=64, flag_mismatches=int((oc != g_conv).sum()))
-    both = oc & g_conv
     if dtype == "f64":
-        assert np.array_equal(oc, g_conv) and np.array_equal(oi, g_it)
-        dq = np.abs(q[both] - ms.q[sel][both]).max()
-        rep["q_max_abs_diff"] = float(dq)
-        assert dq <= 1e-9
+        _c5_fp64_against_pinv(ms, tg, seeds, sel, rep)
     else:
+        q, oc, oi, _ = c_oracle.solve(tg[sel], seeds[ms.best_seed[sel]])
+        rep["flag_mismatches"] = int((oc != g_conv).sum())
+        both = oc & g_conv
         it_off = np.abs(g_it[both] - oi[both])
         ee = _ee_err(solver, q[both], ms.q[sel][both])
         rep.update(iters_outside_pm2=int((it_off > 2).sum()), ee_err_max=float(ee.max()))
         assert rep["flag_mismatches"] <= 1 and rep["iters_outside_pm2"] <= 1 and rep["ee_err_max"] <= 1e-4
-    # a few through the pinv restatement itself (np.linalg.pinv, inverse_geometry.py:83)
-    for j in sel[:4]:
-        qp, okp, itp, _ = o.computeqgrasppose(seeds[best[j]].copy(), tg[j, :9].reshape(3, 3), tg[j, 9:])
-        if dtype == "f64":
-            assert okp == ms.converged[j] and itp == ms.iters[j] and np.abs(qp - ms.q[j]).max() <= 1e-9
-        elif okp and ms.converged[j]:
-            assert abs(itp - int(ms.iters[j])) <= 2
     _report(f"c5_share_{dtype}_v{variant}", rep)
+
+
+def _c5_fp64_against_pinv(ms, tg, seeds, sel, rep):
+    """fp64 from random seeds, against the reference's own step (np.linalg.pinv,
+    inverse_geometry.py:83; oracle/ik_oracle.py), solved on the host's cores.
+    Random seeds start the loop in poorly scaled configurations (cond(J) up to
+    ~5e3 on this sample), so a 1e-16 rounding difference grows along the
+    trajectory: the C oracle's normal equations (cond^2) end 1.3e-8 from the
+    40-digit pinv (oracle.pinv_exact) where numpy's pinv ends 1.3e-9 from it.
+    The kernel's closed form (Sherman-Morrison over the arm blocks, a particular
+    solution projected off J's null vector) has the normal equations' error
+    class, not the SVD's.  Gates: flags and update counts identical except
+    where the stop test is a knife edge (the first run to stop passed it within
+    1e-7 of eps); q within 1e-9 of numpy's pinv on >= 90% of the sample; the
+    worst one no farther from the 40-digit pinv than 4x the C restatement
+    (normal equations) is from it."""
+    from concurrent.futures import ProcessPoolExecutor
+    import multiprocessing as mpc
+    args = [(seeds[ms.best_seed[j]].copy(), tg[j, :9].reshape(3, 3), tg[j, 9:]) for j in sel]
+    with ProcessPoolExecutor(8, mp_context=mpc.get_context("spawn")) as ex:
+        res = list(ex.map(o.computeqgrasppose, *zip(*args)))
+    eps = 1e-3
+    flips, dqs, worst = 0, [], None
+
+    def res_err(q, j):
+        eL, eR = o.hand_errors(q, *o.hook_targets(tg[j, :9].reshape(3, 3), tg[j, 9:]))
+        return np.linalg.norm(eL), np.linalg.norm(eR)
+    for (qp, okp, itp, _), j in zip(res, sel):
+        if okp != ms.converged[j] or itp != ms.iters[j]:
+            # the run that stopped first passed the test by a hair: its error
+            # at the stop is within rounding-growth of eps
+            flips += 1
+            early = float(ms.err[j].max()) if ms.iters[j] < itp else max(res_err(qp, j))
+            margin = eps - early
+            rep.setdefault("knife_edge_margins", []).append(margin)
+            assert 0 <= margin < 1e-7, (int(j), okp, itp, int(ms.iters[j]), margin)
+            continue
+        dq = float(np.abs(qp - ms.q[j]).max())
+        dqs.append(dq)
+        if worst is None or dq > worst[0]:
+            worst = (dq, j, qp)
+    rep.update(knife_edge_flips=flips, q_max_abs_diff_vs_pinv=max(dqs),
+               q_over_1e9=int((np.array(dqs) > 1e-9).sum()))
+    assert flips <= 1
+    assert rep["q_over_1e9"] <= len(sel) // 10, rep
+    dq, j, qp = worst
+    if dq > 1e-9:
+        sd = seeds[ms.best_seed[j]]
+        qx, okx, itx, _ = o.computeqgrasppose(sd.copy(), tg[j, :9].reshape(3, 3), tg[j, 9:], step=o.pinv_exact)
+        qc, _, _, _ = c_oracle.solve(tg[j][None], sd)
+        d_np, d_c, d_gpu = (float(np.abs(x - qx).max()) for x in (qp, qc[0], ms.q[j]))
+        rep.update(worst_target=int(j), worst_seed=int(ms.best_seed[j]), numpy_pinv_vs_exact=d_np,
+                   c_normal_eq_vs_exact=d_c, gpu_vs_exact=d_gpu)
+        assert d_gpu <= 4 * d_c + 1e-10, rep

@@ -266,17 +266,32 @@ def test_multistart_single_seed_broadcasts(solver, variant):
     assert np.array_equal(ms.converged, ref.converged) and (ms.best_seed == 0).all()
 
 
-def test_multistart_nan_target_picks_a_valid_seed(solver):
-    """Every seed of a NaN target has a NaN error: the best-seed reduction must
-    still pick a seed of that target (seed 0), not index past its results."""
+def test_non_finite_host_inputs_are_rejected(solver):
+    """The device code assumes finite math (-ffinite-math-only): host-pointer
+    inputs are checked before staging and a NaN/inf target, q0 row or seed
+    fails with IKG_EINVAL naming the array (include/ikgrasp.h Conventions)."""
+    from ikgrasp._lib import IkgError
     from ikgrasp.workload import uniform_targets, random_seeds
     tg = uniform_targets(3, seed=23)
-    tg[1, 9] = np.nan
     seeds = random_seeds(solver.model, 5, seed=24)
-    ms = solver.solve_multistart(tg, seeds, dtype="f64", max_iters=20)
-    assert ms.best_seed[1] == 0 and not ms.converged[1]
-    ok = solver.solve_multistart(tg[[0, 2]], seeds, dtype="f64", max_iters=20)
-    assert np.array_equal(ms.q[[0, 2]], ok.q) and np.array_equal(ms.best_seed[[0, 2]], ok.best_seed)
+    bad = tg.copy()
+    bad[1, 9] = np.nan
+    for dtype in ("f64", "f32"):
+        with pytest.raises(IkgError, match="targets"):
+            solver.solve(bad, np.zeros(15), dtype=dtype)
+        with pytest.raises(IkgError, match="targets"):
+            solver.solve_multistart(bad, seeds, dtype=dtype)
+        q0 = np.zeros((3, 15))
+        q0[2, 4] = np.inf
+        with pytest.raises(IkgError, match="q0"):
+            solver.solve(tg, q0, dtype=dtype)
+        sd = seeds.copy()
+        sd[3, 7] = -np.inf
+        with pytest.raises(IkgError, match="seeds"):
+            solver.solve_multistart(tg, sd, dtype=dtype)
+    # finite inputs still solve
+    ok = solver.solve_multistart(tg, seeds, dtype="f64", max_iters=20)
+    assert ok.q.shape == (3, 15)
 
 
 def test_torch_q0_shapes_are_checked(solver):
