@@ -213,6 +213,21 @@ IKG_HD inline bool any_of(bool m) { return m; }
 IKG_HD inline bool any_of(v2i m) { return m.x != 0 || m.y != 0; }
 IKG_HD inline bool all_of(bool m) { return m; }
 IKG_HD inline bool all_of(v2i m) { return m.x != 0 && m.y != 0; }
+// Wave-uniform branch conditions (IKG_UNIFORM): a rare per-lane path (exact
+// trig / acos, the near-pi axis) is run by the whole wave when any lane needs
+// it and its result selected per lane, so the branch is a scalar one -- no
+// EXEC save/restore or phi copies on the common path, and every lane's value
+// is the one it computed before (the selects keep the other lanes' results).
+#ifndef IKG_UNIFORM
+#define IKG_UNIFORM 1
+#endif
+IKG_HD inline bool wave_any(bool b) {
+#if defined(__HIP_DEVICE_COMPILE__) && IKG_UNIFORM
+  return __builtin_amdgcn_ballot_w64(b) != 0;
+#else
+  return b;
+#endif
+}
 IKG_HD inline bool mnot(bool m) { return !m; }
 IKG_HD inline v2i mnot(v2i m) { return m == 0; }
 IKG_HD inline bool mor(bool a, bool b) { return a || b; }
@@ -762,12 +777,13 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
       theta = tk->th + ThetaInc<T>::atan_small(fdiv<T>(y, fmax(x, T(1e-30))));
 #endif
     }
-    if (exact) {
+    if (wave_any(exact)) {
 #if IKG_THETA == 1
-      theta = atan2(st, ct);
+      const T th_x = atan2(st, ct);
 #else
-      theta = acos(fmin(fmax(ct, T(-1)), T(1)));  // pin.log3: tr > 3 -> 0, tr < -1 -> pi
+      const T th_x = acos(fmin(fmax(ct, T(-1)), T(1)));  // pin.log3: tr > 3 -> 0, tr < -1 -> pi
 #endif
+      theta = exact ? th_x : theta;
     }
     if (tk) {
       tk->th = theta;
@@ -799,7 +815,7 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
   // cancellation below the near-pi band (there |1+cos| >= 5e-5: < 2e-14 abs.)
   T alpha = hf * (T(1) + ct);
   const M near_pi = theta >= pi - T(1e-2);
-  if (any_of(near_pi)) {  // near pi (rare): the axis from the diagonal
+  if (wave_any(any_of(near_pi))) {  // near pi (rare): the axis from the diagonal
     const T beta = fdiv<T>(t2, T(1) - ct);
     const T t0 = (R[0] - ct) * beta, t1 = (R[4] - ct) * beta, tt = (R[8] - ct) * beta;
     const T wp0 = vsel<T>(R[7] > R[5], T(1), T(-1)) * vsel<T>(t0 > T(0), sqrt(t0), T(0));
@@ -1341,7 +1357,15 @@ IKG_HD inline void trig_advance_f1(const KModel<typename LaneT<T>::E>* __restric
     // common path then needs no register copies to merge the two
 #pragma unroll
     for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
-    if (big) trig_exact_f1(m, arm, qc, qa, sn, cs);
+    if (wave_any(big)) {
+      T se[7], ce[7];
+      trig_exact_f1(m, arm, qc, qa, se, ce);
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        sn[j] = big ? se[j] : sn[j];
+        cs[j] = big ? ce[j] : cs[j];
+      }
+    }
     return;
   }
   T dmax = fabs(d[0]);
@@ -1830,6 +1854,151 @@ IKG_HD inline void arm_pinv7(const T (&A)[6][8], T* z, T* p) {
   }
 }
 
+// The same z_a, p_a from M_a's normal equations, for the guard's usual case:
+// an arm block J_a near singular at the wrist or shoulder, where the chest
+// column keeps M_a = [c_a | J_a] well conditioned (cond ~ 1e2).  G = M_a M_a^T
+// (6 x 6) by Cholesky, y = G^-1 e, w = G^-1 c_a; z = M_a^T y, p = e_0 - M_a^T w.
+// Always in fp64 (a cold branch): the error is ~eps cond(M_a)^2 of the step.
+// It is taken when every Cholesky pivot is >= kNeTol of G's largest diagonal
+// entry (cond(M_a) <~ 1e3: <= ~2e-10 of the step); otherwise (a straight
+// elbow, rank deficiency) the Jacobi form decides the rank as pinv does.
+// ~350 fp64 operations against ~10^4 for the Jacobi sweeps, which made a wave
+// holding a problem that lingers near the wrist several times slower (random
+// seeds, multi-start: round 3).
+constexpr double kNeTol = 1e-6;
+
+IKG_HD inline bool minnorm_ne6x7(const double (&M)[6][7], const double* e, double* z, double* p) {
+  double G[6][6];
+  double gmax = 0.0;
+#pragma unroll
+  for (int r = 0; r < 6; ++r)
+#pragma unroll
+    for (int c = 0; c <= r; ++c) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) acc += M[r][k] * M[c][k];
+      G[r][c] = acc;
+      if (r == c) gmax = acc > gmax ? acc : gmax;
+    }
+  bool ok = true;
+  double rinv[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double d = G[j][j];
+#pragma unroll
+    for (int k = 0; k < j; ++k) d -= G[j][k] * G[j][k];
+    ok = ok && d >= kNeTol * gmax;
+    const double l = sqrt(d > 1e-300 ? d : 1e-300);
+    rinv[j] = 1.0 / l;
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double a = G[i][j];
+#pragma unroll
+      for (int k = 0; k < j; ++k) a -= G[i][k] * G[j][k];
+      G[i][j] = a * rinv[j];
+    }
+  }
+  // forward (L) then backward (L^T) substitution for e and c = M[.][0]
+  double y[6], w[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double a = e[i], b = M[i][0];
+#pragma unroll
+    for (int k = 0; k < i; ++k) {
+      a -= G[i][k] * y[k];
+      b -= G[i][k] * w[k];
+    }
+    y[i] = a * rinv[i];
+    w[i] = b * rinv[i];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double a = y[i], b = w[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; ++k) {
+      a -= G[k][i] * y[k];
+      b -= G[k][i] * w[k];
+    }
+    y[i] = a * rinv[i];
+    w[i] = b * rinv[i];
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    double a = 0.0, b = 0.0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      a += M[r][k] * y[r];
+      b += M[r][k] * w[r];
+    }
+    z[k] = a;
+    p[k] = (k == 0 ? 1.0 : 0.0) - b;
+  }
+  return ok;
+}
+
+// z_a, p_a for one lane (both halves of a packed lane): the normal equations
+// where they are accurate, the Jacobi form elsewhere.  Returns whether every
+// half took the normal equations (diagnostics).
+template <typename T>
+IKG_HD inline bool arm_minnorm(const T (&A)[6][8], T* z, T* p) {
+  constexpr int H = is_packed<T> ? 2 : 1;
+  bool all_ne = true;
+  typename LaneT<T>::M need_j{};
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    auto get = [&](const T& x) -> double {
+      if constexpr (is_packed<T>)
+        return (double)(h == 0 ? x.x : x.y);
+      else
+        return (double)x;
+    };
+    double M[6][7], e[6], zz[7], pp[7];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      M[r][0] = get(A[r][7]);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) M[r][1 + k] = get(A[r][k]);
+      e[r] = get(A[r][6]);
+    }
+    const bool ok = minnorm_ne6x7(M, e, zz, pp);
+    all_ne = all_ne && ok;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      using E = typename LaneT<T>::E;
+      if constexpr (is_packed<T>) {
+        if (h == 0) {
+          z[k].x = (E)zz[k];
+          p[k].x = (E)pp[k];
+        } else {
+          z[k].y = (E)zz[k];
+          p[k].y = (E)pp[k];
+        }
+      } else {
+        z[k] = (E)zz[k];
+        p[k] = (E)pp[k];
+      }
+    }
+    if constexpr (is_packed<T>) {
+      if (h == 0)
+        need_j.x = ok ? 0 : -1;
+      else
+        need_j.y = ok ? 0 : -1;
+    } else {
+      need_j = !ok;
+    }
+  }
+  if (any_of(need_j)) {
+    T zj[7], pj[7];
+    arm_pinv7(A, zj, pj);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      z[k] = vsel(need_j, zj[k], z[k]);
+      p[k] = vsel(need_j, pj[k], p[k]);
+    }
+  }
+  return all_ne;
+}
+
 // The chest value s and this arm's coefficient f (z_a + p_a f) from the two
 // arms' (a, bb) (partner: ao, bbo).  Both lanes of a pair must get the same s
 // bit for bit (each carries the chest joint), so every product is rounded on
@@ -1984,7 +2153,7 @@ __device__ inline void pinv_step_lq(const T (&A)[6][8], int, T* dq, T& s) {
 #ifdef IKG_SING_COUNT
   IKG_SING_TALLY(0, 1);
 #endif
-  arm_pinv7(A, z, p);
+  arm_minnorm(A, z, p);
   minnorm_combine(z[0], p[0], xc(z[0]), xc(p[0]), s, f);
 #pragma unroll
   for (int k = 0; k < 6; ++k) dq[k] = z[1 + k] + f * p[1 + k];

@@ -16,6 +16,7 @@ namespace {
 
 // updates that took the LQ form (pinv_step_*), since the last ikg_emu_lq_count(1)
 thread_local long long lq_count = 0;
+thread_local long long jacobi_count = 0;  // arm solves of the LQ form that fell back to the Jacobi sweeps
 thread_local long long svd_count = 0;  // of those, with an arm that pins the chest (bb = 0: rank-deficient M_a)
 
 // collide_wave's stages run serially (same functions, same order per lane).
@@ -137,7 +138,7 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
         } else {
           arm_system(st[arm], A[arm]);
         }
-        arm_pinv7(A[arm], z[arm], pv[arm]);
+        if (!arm_minnorm(A[arm], z[arm], pv[arm])) ++jacobi_count;
       }
       for (int arm = 0; arm < 2; ++arm) {
         T f;
@@ -212,6 +213,11 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
 extern "C" long long ikg_emu_lq_count(int reset) {
   const long long v = lq_count;
   if (reset) lq_count = 0;
+  return v;
+}
+extern "C" long long ikg_emu_jacobi_count(int reset) {
+  const long long v = jacobi_count;
+  if (reset) jacobi_count = 0;
   return v;
 }
 extern "C" long long ikg_emu_svd_count(int reset) {

@@ -125,6 +125,11 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 #pragma unroll
       for (int i = 0; i < 8; ++i) pad[i] = pad[i] * T(0.999999) + T(1e-7);
 #endif
+#if IKG_UNIFORM
+    // every live lane of the wave has run the same number of updates, so the
+    // count (and the resync / max_iters tests on it) is wave-uniform: scalar
+    it = __builtin_amdgcn_readfirstlane(it);
+#endif
     // fp32: atan2f is as cheap as the tracked angle (measured)
     ThetaTrack<T>* tkp = (IKG_THETA_TRACK && is_f64<T>) ? &tk : nullptr;
     const bool resync = (it % Trig<T>::kResync) == 0;

@@ -29,7 +29,7 @@ def function_spans(path):
     pending = None
     for i, ln in enumerate(open(path), 1):
         s = ln.split("//")[0]
-        if depth <= 1:
+        if depth <= 1 or re.search(r"\binline\b", s):
             m = re.search(r"([A-Za-z_]\w*)\s*\(", s)
             if m and not s.strip().startswith(("if", "for", "while", "return", "#", "static_assert")) and \
                     m.group(1) not in ("if", "for", "while", "switch", "sizeof", "decltype", "alignas"):
@@ -53,26 +53,27 @@ def func_at(spans, line):
     return name
 
 
-SOLVE_STAGES = [  # ikg_solve.hpp solve_pair lines -> stage (by call site)
-    (136, 136, "fk+log6 (arm_fk_error_f1)"),
-    (137, 137, "solve (pinv_step_f1)"),
-    (151, 151, "exchange (pair_swap)"),
-    (152, 180, "stop test"),
-    (181, 185, "update (arm_update)"),
-    (186, 186, "loop counter"),
-    (187, 190, "trig (trig_advance_f1)"),
-]
+_SPANS = {}
 
 
 def stage_of(chain):
-    """chain: list of (file, line) innermost first."""
-    for f, ln in reversed(chain):  # outermost solve_pair frame
-        if f.endswith("ikg_solve.hpp") and 91 <= ln <= 205:
-            for a, b, nm in SOLVE_STAGES:
-                if a <= ln <= b:
-                    return nm
-            return f"solve_pair:{ln}"
-    return "outside solve_pair"
+    """chain: list of (file, line) innermost first.  The stage is the
+    ikg_device.hpp function solve_pair (ikg_solve.hpp) called, or
+    solve_pair:<line> for its own code."""
+    if "dev" not in _SPANS:
+        _SPANS["dev"] = function_spans(os.path.join(CSRC, "ikg_device.hpp"))
+        _SPANS["solve"] = function_spans(os.path.join(CSRC, "ikg_solve.hpp"))
+    idx = [i for i, (f, ln) in enumerate(chain)
+           if f.endswith("ikg_solve.hpp") and func_at(_SPANS["solve"], ln) == "solve_pair"]
+    if not idx:
+        return "outside solve_pair"
+    i = idx[-1]
+    if i == 0:
+        return f"solve_pair:{chain[0][1]}"
+    f, ln = chain[i - 1]
+    if f.endswith("ikg_device.hpp"):
+        return func_at(_SPANS["dev"], ln)
+    return f"{os.path.basename(f)}:{ln}"
 
 
 LOC = re.compile(r";\s*(\S+?):(\d+):\d+(.*)$")
