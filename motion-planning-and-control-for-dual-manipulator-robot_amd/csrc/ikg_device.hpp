@@ -1857,52 +1857,56 @@ IKG_HD inline void arm_pinv7(const T (&A)[6][8], T* z, T* p) {
 // The same z_a, p_a from M_a's normal equations, for the guard's usual case:
 // an arm block J_a near singular at the wrist or shoulder, where the chest
 // column keeps M_a = [c_a | J_a] well conditioned (cond ~ 1e2).  G = M_a M_a^T
-// (6 x 6) by Cholesky, y = G^-1 e, w = G^-1 c_a; z = M_a^T y, p = e_0 - M_a^T w.
-// Always in fp64 (a cold branch): the error is ~eps cond(M_a)^2 of the step.
-// It is taken when every Cholesky pivot is >= kNeTol of G's largest diagonal
-// entry (cond(M_a) <~ 1e3: <= ~2e-10 of the step); otherwise (a straight
-// elbow, rank deficiency) the Jacobi form decides the rank as pinv does.
-// ~350 fp64 operations against ~10^4 for the Jacobi sweeps, which made a wave
-// holding a problem that lingers near the wrist several times slower (random
-// seeds, multi-start: round 3).
+// (6 x 6) by Cholesky, y = G^-1 e, w = G^-1 c_a; z = M_a^T y, p = e_0 - M_a^T w,
+// in the lane type (packed: both arms at once).  The error is ~eps
+// cond(M_a)^2 of the step; it is taken where every Cholesky pivot is >= kNeTol
+// of G's largest diagonal entry (cond(M_a) <~ 1e3: fp64 <= ~2e-10 of the step,
+// fp32 below the closed form's own error at its guard bound); elsewhere (a
+// straight elbow, rank deficiency) the Jacobi form decides the rank as pinv
+// does.  ~350 operations against ~10^4 for the Jacobi sweeps, which made a
+// wave holding a problem that lingers near the wrist several times slower
+// (random seeds, multi-start: round 3).
 constexpr double kNeTol = 1e-6;
 
-IKG_HD inline bool minnorm_ne6x7(const double (&M)[6][7], const double* e, double* z, double* p) {
-  double G[6][6];
-  double gmax = 0.0;
+template <typename T>
+IKG_HD inline typename LaneT<T>::M minnorm_ne(const T (&A)[6][8], T* z, T* p) {
+  using E = typename LaneT<T>::E;
+  // rows of M_a = [c | J_a]: column 0 = chest (A[.][7]), 1..6 = A[.][0..5]
+  auto M = [&](int r, int k) -> T { return k == 0 ? A[r][7] : A[r][k - 1]; };
+  T G[6][6];
+  T gmax = T(0);
 #pragma unroll
   for (int r = 0; r < 6; ++r)
 #pragma unroll
     for (int c = 0; c <= r; ++c) {
-      double acc = 0.0;
+      T acc = T(0);
 #pragma unroll
-      for (int k = 0; k < 7; ++k) acc += M[r][k] * M[c][k];
+      for (int k = 0; k < 7; ++k) acc += M(r, k) * M(c, k);
       G[r][c] = acc;
-      if (r == c) gmax = acc > gmax ? acc : gmax;
+      if (r == c) gmax = tmax(gmax, acc);
     }
-  bool ok = true;
-  double rinv[6];
+  auto ok = gmax > T(0);
+  T rinv[6];
 #pragma unroll
   for (int j = 0; j < 6; ++j) {
-    double d = G[j][j];
+    T d = G[j][j];
 #pragma unroll
     for (int k = 0; k < j; ++k) d -= G[j][k] * G[j][k];
-    ok = ok && d >= kNeTol * gmax;
-    const double l = sqrt(d > 1e-300 ? d : 1e-300);
-    rinv[j] = 1.0 / l;
+    ok = ok & (d >= T(E(kNeTol)) * gmax);
+    rinv[j] = fdiv(T(1), tsqrt(tmax(d, T(E(Prec<E>::kRcond)) * gmax + T(E(1e-30)))));
 #pragma unroll
     for (int i = j + 1; i < 6; ++i) {
-      double a = G[i][j];
+      T a = G[i][j];
 #pragma unroll
       for (int k = 0; k < j; ++k) a -= G[i][k] * G[j][k];
       G[i][j] = a * rinv[j];
     }
   }
   // forward (L) then backward (L^T) substitution for e and c = M[.][0]
-  double y[6], w[6];
+  T y[6], w[6];
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
-    double a = e[i], b = M[i][0];
+    T a = A[i][6], b = A[i][7];
 #pragma unroll
     for (int k = 0; k < i; ++k) {
       a -= G[i][k] * y[k];
@@ -1913,7 +1917,7 @@ IKG_HD inline bool minnorm_ne6x7(const double (&M)[6][7], const double* e, doubl
   }
 #pragma unroll
   for (int i = 5; i >= 0; --i) {
-    double a = y[i], b = w[i];
+    T a = y[i], b = w[i];
 #pragma unroll
     for (int k = i + 1; k < 6; ++k) {
       a -= G[k][i] * y[k];
@@ -1924,14 +1928,14 @@ IKG_HD inline bool minnorm_ne6x7(const double (&M)[6][7], const double* e, doubl
   }
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
-    double a = 0.0, b = 0.0;
+    T a = T(0), b = T(0);
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-      a += M[r][k] * y[r];
-      b += M[r][k] * w[r];
+      a += M(r, k) * y[r];
+      b += M(r, k) * w[r];
     }
     z[k] = a;
-    p[k] = (k == 0 ? 1.0 : 0.0) - b;
+    p[k] = (k == 0 ? T(1) : T(0)) - b;
   }
   return ok;
 }
@@ -1941,52 +1945,8 @@ IKG_HD inline bool minnorm_ne6x7(const double (&M)[6][7], const double* e, doubl
 // half took the normal equations (diagnostics).
 template <typename T>
 IKG_HD inline bool arm_minnorm(const T (&A)[6][8], T* z, T* p) {
-  constexpr int H = is_packed<T> ? 2 : 1;
-  bool all_ne = true;
-  typename LaneT<T>::M need_j{};
-#pragma unroll
-  for (int h = 0; h < H; ++h) {
-    auto get = [&](const T& x) -> double {
-      if constexpr (is_packed<T>)
-        return (double)(h == 0 ? x.x : x.y);
-      else
-        return (double)x;
-    };
-    double M[6][7], e[6], zz[7], pp[7];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) {
-      M[r][0] = get(A[r][7]);
-#pragma unroll
-      for (int k = 0; k < 6; ++k) M[r][1 + k] = get(A[r][k]);
-      e[r] = get(A[r][6]);
-    }
-    const bool ok = minnorm_ne6x7(M, e, zz, pp);
-    all_ne = all_ne && ok;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      using E = typename LaneT<T>::E;
-      if constexpr (is_packed<T>) {
-        if (h == 0) {
-          z[k].x = (E)zz[k];
-          p[k].x = (E)pp[k];
-        } else {
-          z[k].y = (E)zz[k];
-          p[k].y = (E)pp[k];
-        }
-      } else {
-        z[k] = (E)zz[k];
-        p[k] = (E)pp[k];
-      }
-    }
-    if constexpr (is_packed<T>) {
-      if (h == 0)
-        need_j.x = ok ? 0 : -1;
-      else
-        need_j.y = ok ? 0 : -1;
-    } else {
-      need_j = !ok;
-    }
-  }
+  const auto ok = minnorm_ne(A, z, p);
+  const auto need_j = mnot(ok);
   if (any_of(need_j)) {
     T zj[7], pj[7];
     arm_pinv7(A, zj, pj);
@@ -1996,7 +1956,7 @@ IKG_HD inline bool arm_minnorm(const T (&A)[6][8], T* z, T* p) {
       p[k] = vsel(need_j, pj[k], p[k]);
     }
   }
-  return all_ne;
+  return !any_of(need_j);
 }
 
 // The chest value s and this arm's coefficient f (z_a + p_a f) from the two
