@@ -221,12 +221,14 @@ IKG_HD inline bool all_of(v2i m) { return m.x != 0 && m.y != 0; }
 #ifndef IKG_UNIFORM
 #define IKG_UNIFORM 1
 #endif
+// Not for the packed fp32 layout: there the scalar branches cost 2-3% at C3
+// under its max-ILP schedule (round 3 A/B), so T = v2f keeps per-lane ones.
+template <typename T>
 IKG_HD inline bool wave_any(bool b) {
 #if defined(__HIP_DEVICE_COMPILE__) && IKG_UNIFORM
-  return __builtin_amdgcn_ballot_w64(b) != 0;
-#else
-  return b;
+  if constexpr (!LaneT<T>::packed) return __builtin_amdgcn_ballot_w64(b) != 0;
 #endif
+  return b;
 }
 IKG_HD inline bool mnot(bool m) { return !m; }
 IKG_HD inline v2i mnot(v2i m) { return m == 0; }
@@ -777,7 +779,7 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
       theta = tk->th + ThetaInc<T>::atan_small(fdiv<T>(y, fmax(x, T(1e-30))));
 #endif
     }
-    if (wave_any(exact)) {
+    if (wave_any<T>(exact)) {
 #if IKG_THETA == 1
       const T th_x = atan2(st, ct);
 #else
@@ -815,7 +817,7 @@ IKG_HD inline void log6_iter(const T* R, const T* p, T* e, ThetaTrack<T>* tk = n
   // cancellation below the near-pi band (there |1+cos| >= 5e-5: < 2e-14 abs.)
   T alpha = hf * (T(1) + ct);
   const M near_pi = theta >= pi - T(1e-2);
-  if (wave_any(any_of(near_pi))) {  // near pi (rare): the axis from the diagonal
+  if (wave_any<T>(any_of(near_pi))) {  // near pi (rare): the axis from the diagonal
     const T beta = fdiv<T>(t2, T(1) - ct);
     const T t0 = (R[0] - ct) * beta, t1 = (R[4] - ct) * beta, tt = (R[8] - ct) * beta;
     const T wp0 = vsel<T>(R[7] > R[5], T(1), T(-1)) * vsel<T>(t0 > T(0), sqrt(t0), T(0));
@@ -1357,7 +1359,7 @@ IKG_HD inline void trig_advance_f1(const KModel<typename LaneT<T>::E>* __restric
     // common path then needs no register copies to merge the two
 #pragma unroll
     for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
-    if (wave_any(big)) {
+    if (wave_any<T>(big)) {
       T se[7], ce[7];
       trig_exact_f1(m, arm, qc, qa, se, ce);
 #pragma unroll
@@ -2119,6 +2121,26 @@ __device__ inline void pinv_step_lq(const T (&A)[6][8], int, T* dq, T& s) {
   for (int k = 0; k < 6; ++k) dq[k] = z[1 + k] + f * p[1 + k];
 }
 
+// The guard's branch as an out-of-line call (IKG_COLD_CALL): the loop is then
+// register-allocated as if the branch did not exist, and only a taken branch
+// pays for saving the loop's state around the call (round 3: the inlined
+// branch cost the never-taken loop 3-4% at C2 / C3).
+#ifndef IKG_COLD_CALL
+#define IKG_COLD_CALL 1
+#endif
+template <typename T>
+struct ColdIO {  // the branch's inputs and outputs, copied only when it is taken
+  ArmStateF1<T> st;
+  T sn[7], cs[7], dq[6], s;
+};
+template <typename T, class SP, class X>
+__device__ __attribute__((noinline)) void pinv_step_f1_cold(const KModel<typename LaneT<T>::E>* __restrict__ m,
+                                                            int arm, ColdIO<T>* io) {
+  T A[6][8];
+  arm_system_f1<T, SP>(m, arm, io->st, io->sn, io->cs, A);
+  pinv_step_lq<T, X>(A, arm, io->dq, io->s);
+}
+
 template <typename T, class SP, class X = PairX>
 __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
                                     const T* sn, const T* cs, T* dq, T& s) {
@@ -2127,6 +2149,22 @@ __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restri
   bool need;
   pinv_step_tail<T, X>(u, v, alpha, beta, m->sing_beta, dq, s, need);
   if (__builtin_expect(IKG_SING_GUARD && need, 0)) {
+#if IKG_COLD_CALL
+    if constexpr (is_f64<T>) {  // fp64 only: the fp32 kernels measured 2-10% slower with the call
+      ColdIO<T> io;
+      io.st = st;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        io.sn[j] = sn[j];
+        io.cs[j] = cs[j];
+      }
+      pinv_step_f1_cold<T, SP, X>(m, arm, &io);
+#pragma unroll
+      for (int k = 0; k < 6; ++k) dq[k] = io.dq[k];
+      s = io.s;
+      return;
+    }
+#endif
     T A[6][8];
     arm_system_f1<T, SP>(m, arm, st, sn, cs, A);
     pinv_step_lq<T, X>(A, arm, dq, s);

@@ -128,7 +128,7 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 #if IKG_UNIFORM
     // every live lane of the wave has run the same number of updates, so the
     // count (and the resync / max_iters tests on it) is wave-uniform: scalar
-    it = __builtin_amdgcn_readfirstlane(it);
+    if constexpr (!is_packed<T>) it = __builtin_amdgcn_readfirstlane(it);
 #endif
     // fp32: atan2f is as cheap as the tracked angle (measured)
     ThetaTrack<T>* tkp = (IKG_THETA_TRACK && is_f64<T>) ? &tk : nullptr;

@@ -32,10 +32,21 @@ cv = torch.empty(B, dtype=torch.uint8, device=dev)
 it = torch.empty(B, dtype=torch.int32, device=dev)
 er = torch.empty((B, 2), dtype=tdt, device=dev)
 desc = _lib.model_desc(load_nextage())
+# ABL_MS=S: multi-start (BASELINE configs[4]): B targets x S random seeds (seed 0 = q0 = 0)
+MS = int(os.environ.get("ABL_MS", "0"))
+if MS:
+    from ikgrasp.workload import random_seeds  # noqa: E402
+    sd = random_seeds(load_nextage(), MS, seed=1001)
+    sd[0] = 0.0
+    seeds = torch.tensor(sd, dtype=tdt, device=dev)
+    best = torch.empty(B, dtype=torch.int32, device=dev)
 handles = []
 for p in libs:
     lib = C.CDLL(p)
     lib.ikg_model_create.argtypes = [C.POINTER(_lib.ModelDesc), C.POINTER(C.c_void_p)]
+    lib.ikg_solve_multistart.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64,
+                                         C.POINTER(_lib.Params), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_uint32]
     lib.ikg_solve_batch.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
                                     C.POINTER(_lib.Params), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_uint32]
@@ -49,6 +60,17 @@ times = {n: [] for n, _, _ in handles}
 for rnd in range(int(os.environ.get("ABL_ROUNDS", "6"))):
     for n, lib, h in handles:
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if MS:
+            a.record()
+            rc = lib.ikg_solve_multistart(h, 0, code, tg.data_ptr(), B, seeds.data_ptr(), MS, C.byref(prm),
+                                          qo.data_ptr(), cv.data_ptr(), it.data_ptr(), er.data_ptr(), best.data_ptr(),
+                                          C.c_void_p(s), 0)
+            b.record()
+            torch.cuda.synchronize()
+            assert rc == 0
+            if rnd > 0:
+                times[n].append(a.elapsed_time(b))
+            continue
         a.record()
         rc = lib.ikg_solve_batch(h, 0, code, tg.data_ptr(), q0.data_ptr(), 0 if q0.dim() == 1 else 15, B, C.byref(prm), qo.data_ptr(),
                                  cv.data_ptr(), it.data_ptr(), er.data_ptr(), C.c_void_p(s), 0)
