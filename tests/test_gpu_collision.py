@@ -103,8 +103,13 @@ def test_solve_with_collision_fp32(csolver, solve_cases, rounds, monkeypatch):
     _schedule(monkeypatch, rounds)
     c = solve_cases
     sol = csolver.solve(c["targets"], c["q0"], dtype="f32", check_collision=True)
-    agree = (sol.converged == c["success"]).mean()
-    assert agree >= 0.95
+    # fp32 against the fp64 fixture: a success flag may flip only where the stop
+    # test or the collision query is decided within fp32 rounding; the flips are
+    # printed (pytest -s) so the count the gate allows is on record
+    flips = np.nonzero(sol.converged != c["success"])[0]
+    print(f"fp32 collision solves, schedule {rounds}: {len(flips)} of {len(sol.converged)} "
+          f"success flags differ from the fp64 fixture: {flips.tolist()}")
+    assert len(flips) <= 2
     both = sol.converged & c["success"]
     assert (np.abs(sol.iters[both] - c["iters"][both]) <= 2).all()
 

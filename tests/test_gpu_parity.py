@@ -123,9 +123,13 @@ def test_config_b65536_fp32_vs_fp64(solver):
     s32 = solver.solve(tg, np.zeros(15), dtype="f32")
     s64 = solver.solve(tg, np.zeros(15), dtype="f64")
     both = s32.converged & s64.converged
-    agree = (s32.converged == s64.converged).mean()
-    assert agree >= 0.995
-    assert (np.abs(s32.iters[both].astype(int) - s64.iters[both]) <= 2).mean() >= 0.99
+    flips = int((s32.converged != s64.converged).sum())
+    off = int((np.abs(s32.iters[both].astype(int) - s64.iters[both]) > 2).sum())
+    # printed (pytest -s) so the escapes the gates allow are on record; the
+    # oracle-side comparison of this config is tests/test_gpu_configs.py
+    print(f"C3 fp32 vs fp64 on 65,536: {flips} flag flips, {off} of {int(both.sum())} update counts outside +-2")
+    assert flips <= 0.005 * len(tg)
+    assert off <= 0.01 * both.sum()
     h32 = solver.fk(s32.q.astype(np.float64))
     h64 = solver.fk(s64.q)
     for h in range(2):
