@@ -109,7 +109,7 @@ def test_solve_with_collision_fp32(csolver, solve_cases, rounds, monkeypatch):
     flips = np.nonzero(sol.converged != c["success"])[0]
     print(f"fp32 collision solves, schedule {rounds}: {len(flips)} of {len(sol.converged)} "
           f"success flags differ from the fp64 fixture: {flips.tolist()}")
-    assert len(flips) <= 2
+    assert len(flips) <= 1  # measured 0 of 96 in every schedule (round 3)
     both = sol.converged & c["success"]
     assert (np.abs(sol.iters[both] - c["iters"][both]) <= 2).all()
 

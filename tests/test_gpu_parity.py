@@ -128,8 +128,8 @@ def test_config_b65536_fp32_vs_fp64(solver):
     # printed (pytest -s) so the escapes the gates allow are on record; the
     # oracle-side comparison of this config is tests/test_gpu_configs.py
     print(f"C3 fp32 vs fp64 on 65,536: {flips} flag flips, {off} of {int(both.sum())} update counts outside +-2")
-    assert flips <= 0.005 * len(tg)
-    assert off <= 0.01 * both.sum()
+    assert flips <= 0.001 * len(tg)  # measured 0 (round 3)
+    assert off <= 0.002 * both.sum()  # measured 0 of 26,570
     h32 = solver.fk(s32.q.astype(np.float64))
     h64 = solver.fk(s64.q)
     for h in range(2):
