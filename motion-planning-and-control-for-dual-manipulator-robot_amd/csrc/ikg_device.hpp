@@ -2141,7 +2141,9 @@ __device__ __attribute__((noinline)) void pinv_step_f1_cold(const KModel<typenam
   pinv_step_lq<T, X>(A, arm, io->dq, io->s);
 }
 
-template <typename T, class SP, class X = PairX>
+// COLD: the out-of-line branch (fp64 only); the records-in-batch loop (REC)
+// measured 3% slower with it at C2 with the collision term, so it inlines
+template <typename T, class SP, class X = PairX, bool COLD = true>
 __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
                                     const T* sn, const T* cs, T* dq, T& s) {
   T u[6], v[6], alpha, beta;
@@ -2150,7 +2152,7 @@ __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restri
   pinv_step_tail<T, X>(u, v, alpha, beta, m->sing_beta, dq, s, need);
   if (__builtin_expect(IKG_SING_GUARD && need, 0)) {
 #if IKG_COLD_CALL
-    if constexpr (is_f64<T>) {  // fp64 only: the fp32 kernels measured 2-10% slower with the call
+    if constexpr (is_f64<T> && COLD) {  // fp64 only: the fp32 kernels measured 2-10% slower with the call
       ColdIO<T> io;
       io.st = st;
 #pragma unroll

@@ -139,7 +139,7 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     if constexpr (F1) {
       ArmStateF1<T> st;
       x = arm_fk_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, tkp, resync);
-      pinv_step_f1<T, SP>(m, arm, st, sn, cs, dq, s);
+      pinv_step_f1<T, SP, PairX, !REC>(m, arm, st, sn, cs, dq, s);
     } else {
     ArmState<T> st;
     x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, tkp, resync);

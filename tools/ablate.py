@@ -32,6 +32,10 @@ cv = torch.empty(B, dtype=torch.uint8, device=dev)
 it = torch.empty(B, dtype=torch.int32, device=dev)
 er = torch.empty((B, 2), dtype=tdt, device=dev)
 desc = _lib.model_desc(load_nextage())
+COL = bool(int(os.environ.get("ABL_COLLISION", "0")))
+if COL:
+    from ikgrasp.collision import load_nextage_scene  # noqa: E402
+    cdesc = _lib.collision_desc(load_nextage_scene())
 # ABL_MS=S: multi-start (BASELINE configs[4]): B targets x S random seeds (seed 0 = q0 = 0)
 MS = int(os.environ.get("ABL_MS", "0"))
 if MS:
@@ -52,9 +56,12 @@ for p in libs:
                                     C.c_void_p, C.c_uint32]
     h = C.c_void_p()
     assert lib.ikg_model_create(C.byref(desc), C.byref(h)) == 0
+    if COL:  # ABL_COLLISION=1: the solve with the collision term (its whole kernel sequence is timed)
+        lib.ikg_model_set_collision.argtypes = [C.c_void_p, C.POINTER(_lib.CollisionDesc)]
+        assert lib.ikg_model_set_collision(h, C.byref(cdesc)) == 0
     handles.append((os.path.relpath(p, ROOT)[-40:], lib, h))
 prm = _lib.Params(eps=float(os.environ.get("ABL_EPS", "1e-37")), dt=1e-2, max_iters=1000,
-                  variant=int(os.environ.get("ABL_VARIANT", "0")), lambda_=0.0)
+                  variant=int(os.environ.get("ABL_VARIANT", "0")), lambda_=0.0, check_collision=int(COL))
 s = torch.cuda.current_stream().cuda_stream
 times = {n: [] for n, _, _ in handles}
 for rnd in range(int(os.environ.get("ABL_ROUNDS", "6"))):
