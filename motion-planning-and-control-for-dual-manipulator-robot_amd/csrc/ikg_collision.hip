@@ -78,6 +78,9 @@ __device__ unsigned long long g_wprof[6];
 // wave-wide rounds of 64 with an early exit on the first round holding a hit,
 // whose lowest pair becomes the new witness.  The result is the OR over all
 // active pairs either way: only the order of the tests changes.
+#ifndef IKG_SWEEP_COMPACT
+#define IKG_SWEEP_COMPACT 1
+#endif
 template <typename T, bool WITNESS>
 __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
                              CollideScratch<T>& S, const T* tgt, Witness<T>& W,
@@ -127,6 +130,43 @@ __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T
   for (int g = lane; g < c->n_geoms; g += 64) geom_world(c, g, S.F, tgt, S.P[g]);
   __syncthreads();
   bool found = false;
+#if IKG_SWEEP_COMPACT
+  // Two passes: the bounding-sphere test of every pair, the survivors listed
+  // in pair order (ballot + popcount), then the exact tests over the list in
+  // rounds of 64.  A collision-free pose runs ~2 narrow-phase rounds instead of
+  // a GJK-latency round in each of the 12 rounds of 64 pairs; the answer and
+  // the witness (lowest colliding pair) are the single pass's.
+  int ncand = 0;
+  for (int base = 0; base < c->n_pairs; base += 64) {
+    const int k = base + lane;
+    bool pass = false;
+    if (k < c->n_pairs && k != w) {
+      const int a = c->pairs[k][0], b = c->pairs[k][1];
+      const T d0 = S.P[a][9] - S.P[b][9], d1 = S.P[a][10] - S.P[b][10], d2 = S.P[a][11] - S.P[b][11];
+      const T r = c->brad[a] + c->brad[b];
+      pass = d0 * d0 + d1 * d1 + d2 * d2 < r * r;
+    }
+    const unsigned long long bal = __ballot(pass);
+    if (pass) S.cand[ncand + __popcll(bal & ((1ull << lane) - 1))] = (int16_t)k;
+    ncand += __popcll(bal);
+  }
+  __syncthreads();
+  for (int base = 0; base < ncand; base += 64) {
+    const int i = base + lane;
+    const int k = i < ncand ? S.cand[i] : 0;
+    bool hit = false;
+    if (i < ncand) {
+      const int a = c->pairs[k][0], b = c->pairs[k][1];
+      hit = pair_collides(pair_shape(c, a, S.P), pair_shape(c, b, S.P)) != 0;
+    }
+    const unsigned long long bal = __ballot(hit);
+    if (bal) {
+      if (WITNESS && lane == 0) W.pair = S.cand[base + __ffsll((long long)bal) - 1];
+      found = true;
+      break;
+    }
+  }
+#else
   for (int base = 0; base < c->n_pairs; base += 64) {
     const int k = base + lane;
     const bool hit = k < c->n_pairs && k != w && pair_hit(c, k, S.P) != 0;
@@ -137,6 +177,7 @@ __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T
       break;
     }
   }
+#endif
   if (WITNESS && lane == 0) {
     if (!found) W.pair = -1;
     W.cert_ok = 0;

@@ -44,6 +44,7 @@ struct CollideScratch {
   T L[kMaxNq][12];   // joint-local transforms placement * R_axis(q)
   T F[kMaxNq][12];   // world joint frames
   T P[kMaxGeoms][12];  // world geometry placements
+  int16_t cand[kMaxPairs];  // pairs past the bounding-sphere test, in pair order (collide_wave)
 };
 
 // Expanding-polytope scratch (epa_depth_lb): at most kEpaIters expansions of
