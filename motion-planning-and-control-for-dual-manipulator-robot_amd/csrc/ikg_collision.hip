@@ -1466,47 +1466,71 @@ __device__ __forceinline__ void traj_window(const KModel<T>* __restrict__ m, con
 }
 
 // Does pair `pair` intersect at configuration q (a record row)?  One lane's
-// own test: the two geometries' placements from their joint chains (leaf to
-// root, left-multiplying the local transforms), then the narrow phase.
+// own test: the two geometries' placements from their joint chains, then the
+// narrow phase.  The chains' common part (the lowest common ancestor joint up
+// to the root) is built once: each branch is accumulated leaf to LCA
+// (left-multiplying the local transforms), then left-multiplied by the shared
+// product (round 3: the witness pairs are mostly on one arm, where the shared
+// part was half of the per-record sincos and products).
+template <typename T>
+__device__ inline void chain_mul(const KModel<T>* __restrict__ m, const T* __restrict__ q, const int32_t* sl, int from,
+                                 int stop, T (&F)[12]) {
+  for (int k = from; k != stop; k = m->jparent[k]) {
+    T L[12], Rn[9], tn[3], sk, ck;
+    Prec<T>::sincos_(q[sl[k]], &sk, &ck);
+    joint_local(m, k, sk, ck, L);
+    matmul3(L, F, Rn);
+    matvec3(L, F + 9, tn);
+    for (int i = 0; i < 9; ++i) F[i] = Rn[i];
+    for (int i = 0; i < 3; ++i) F[9 + i] = L[9 + i] + tn[i];
+  }
+}
+
 template <typename T>
 __device__ inline bool witness_hit_lane(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
                                         int pair, const T* __restrict__ q, const int32_t* sl, const T* tgt,
                                         T (*P)[12]) {
+  const int gg[2] = {c->pairs[pair][0], c->pairs[pair][1]};
+  int jj[2];
+  for (int h = 0; h < 2; ++h) jj[h] = gg[h] == c->target_geom ? -1 : c->joint[gg[h]];
+  // lowest common ancestor of the two joints (-1: none)
+  int lca = -1;
+  if (jj[0] >= 0 && jj[1] >= 0) {
+    uint32_t anc = 0;
+    for (int k = jj[0]; k >= 0; k = m->jparent[k]) anc |= 1u << k;
+    lca = jj[1];
+    while (lca >= 0 && !((anc >> lca) & 1u)) lca = m->jparent[lca];
+  }
+  T Fs[12] = {T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0)};
+  if (lca >= 0) chain_mul(m, q, sl, lca, -1, Fs);
   for (int h = 0; h < 2; ++h) {
-    const int g = c->pairs[pair][h];
+    const int g = gg[h];
     if (g == c->target_geom) {
       for (int i = 0; i < 12; ++i) P[h][i] = tgt[i];
       continue;
     }
-    int j = c->joint[g];
+    const int j = jj[h];
     if (j < 0) {
       for (int i = 0; i < 9; ++i) P[h][i] = c->R[g][i];
       for (int i = 0; i < 3; ++i) P[h][9 + i] = c->t[g][i];
       continue;
     }
-    T F[12];
-    {
-      T sj, cj;
-      Prec<T>::sincos_(q[sl[j]], &sj, &cj);
-      joint_local(m, j, sj, cj, F);
-    }
-    for (int k = m->jparent[j]; k >= 0; k = m->jparent[k]) {
-      T L[12], Rn[9], tn[3], sk, ck;
-      Prec<T>::sincos_(q[sl[k]], &sk, &ck);
-      joint_local(m, k, sk, ck, L);
-      matmul3(L, F, Rn);
-      matvec3(L, F + 9, tn);
+    T F[12] = {T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0)};
+    chain_mul(m, q, sl, j, lca, F);  // leaf up to (not including) the LCA, or to the root
+    if (lca >= 0) {
+      T Rn[9], tn[3];
+      matmul3(Fs, F, Rn);
+      matvec3(Fs, F + 9, tn);
       for (int i = 0; i < 9; ++i) F[i] = Rn[i];
-      for (int i = 0; i < 3; ++i) F[9 + i] = L[9 + i] + tn[i];
+      for (int i = 0; i < 3; ++i) F[9 + i] = Fs[9 + i] + tn[i];
     }
     T tn[3];
     matmul3(F, c->R[g], P[h]);
     matvec3(F, c->t[g], tn);
     for (int i = 0; i < 3; ++i) P[h][9 + i] = F[9 + i] + tn[i];
   }
-  const int ga = c->pairs[pair][0], gb = c->pairs[pair][1];
-  const Shape<T> A{P[0], P[0] + 9, c->dims[ga], c->kind[ga]};
-  const Shape<T> B{P[1], P[1] + 9, c->dims[gb], c->kind[gb]};
+  const Shape<T> A{P[0], P[0] + 9, c->dims[gg[0]], c->kind[gg[0]]};
+  const Shape<T> B{P[1], P[1] + 9, c->dims[gg[1]], c->kind[gg[1]]};
   return pair_collides(A, B) != 0;
 }
 

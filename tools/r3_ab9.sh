@@ -1,0 +1,7 @@
+#!/bin/bash
+ROOT=$(pwd); O=$ROOT/gpurun_out/ab9; mkdir -p $O
+L="$ROOT/ab_libs/*.so"
+ABL_COLLISION=1 ABL_MS=256 ABL_EPS=1e-3 ABL_ROUNDS=6 timeout -k 10 300 python tools/ablate.py 512 f32 "$L" > $O/c5col_f32.txt 2>&1 || exit 3
+ABL_COLLISION=1 ABL_MS=256 ABL_EPS=1e-3 ABL_ROUNDS=4 timeout -k 10 300 python tools/ablate.py 512 f64 "$L" > $O/c5col_f64.txt 2>&1 || exit 3
+ABL_COLLISION=1 ABL_EPS=1e-3 ABL_ROUNDS=4 timeout -k 10 300 python tools/ablate.py 131072 f64 "$L" > $O/c4scol_f64.txt 2>&1 || exit 3
+grep -H median $O/*.txt
