@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 3 evidence refresh: GPU tests, smoke, bench lines (C2 default with extras and CPU
 # legs, C3, C4 share, C5 share, collision), rocprofv3 kernel-trace summaries, PMC passes.
-ROOT=$(pwd); O=$ROOT/gpurun_out/refresh3; mkdir -p $O; export TMPDIR=/tmp
+ROOT=$(pwd); O=$ROOT/gpurun_out/${RTAG:-refresh3}; mkdir -p $O; export TMPDIR=/tmp
 fatal() { case $1 in 0) return 0;; *) echo "FATAL $2 rc=$1" | tee -a $O/summary.txt; exit $1;; esac; }
 IKG_REPORT_DIR=$O/reports timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?
 grep -E "passed|failed" $O/pytest_gpu.log | tail -1 | tee -a $O/summary.txt; [ $rc -le 1 ] || exit $rc
