@@ -58,6 +58,20 @@ __device__ __forceinline__ void store_block8(T* dst, const T (&v)[8]) {
   }
 }
 
+template <typename T>
+__device__ __forceinline__ void load_block8(const T* src, T (&v)[8]) {
+  struct alignas(16) V16 {
+    T x[16 / sizeof(T)];
+  };
+  constexpr int per = 16 / (int)sizeof(T);
+#pragma unroll
+  for (int k = 0; k < 8 / per; ++k) {
+    const V16 b = reinterpret_cast<const V16*>(src)[k];
+#pragma unroll
+    for (int e = 0; e < per; ++e) v[k * per + e] = b.x[e];
+  }
+}
+
 // Record-in-batch outputs of one problem (ikg_pair_batch_kernel with REC):
 // the loop goes on past the first iterate whose errors pass, recording every
 // iterate for the collision scan; that iterate's outputs are stored when reached.
@@ -157,15 +171,9 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     if constexpr (REC) {
       const bool ended = it >= prm.max_iters;  // never tested (:56 loop exhausted)
       const bool pass = !ended && both_below(x, xo, prm.eps2);
-      if (pass && k0 < 0) {  // the answer unless it collides: stored now, the loop goes on
+      if (pass && k0 < 0) {  // the answer unless it collides: record 0, written out after the loop
         k0 = it;
         conv = true;
-        store_q(m, arm, ro->qrow, it, qc, qa, ro->qo);
-        ro->err[arm] = sqrt(x);
-        if (arm == 0) {
-          *ro->conv = 1;
-          *ro->iters = it;
-        }
       }
       if (k0 >= 0) {
         T blk[8];
@@ -201,7 +209,23 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   if (any_of(ps == T(-12345.678))) it = -1;  // never true; keeps the padding live
 #endif
   if constexpr (REC) {
-    if (k0 >= 0 && arm == 0) *ro->nrec = (it - k0 + 1) | kTrajEnded;
+    if (k0 >= 0) {
+      // the outputs at the first passing iterate, from its record (this lane's
+      // own block of record 0): writing them inside the loop put a divergent
+      // branch into every update (records-in-batch kernel 4% slower)
+      T blk[8];
+      load_block8(ro->rec + (arm ? kRecPass : kRecRoot), blk);
+      T qa0[kArmDof];
+#pragma unroll
+      for (int k = 0; k < kArmDof; ++k) qa0[k] = blk[1 + k];
+      store_q(m, arm, ro->qrow, k0, blk[0], qa0, ro->qo);
+      ro->err[arm] = sqrt(blk[7]);
+      if (arm == 0) {
+        *ro->conv = 1;
+        *ro->iters = k0;
+        *ro->nrec = (it - k0 + 1) | kTrajEnded;
+      }
+    }
   }
   it_out = it;
   nrm_out = sqrt(x);
