@@ -1992,7 +1992,8 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     tw.by_p = 1;
     ws_trace("alloc scan", dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     poison_int(dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
-    hipLaunchKernelGGL(ikg_fill_i32_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s, tw.done, a.B, 0);
+    // one scan round with the pre-screen's witnesses: `done` is only written
+    // (read by later rounds, of which there are none here), so it needs no fill
     hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)std::min<int64_t>(1024, a.B)), dim3(64), 0, s, dm, dc,
                        (const T*)a.targets, a.S, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
                        (const int32_t*)w.wit, tw, prm.max_iters + 1, 0, (T*)a.q_out, a.converged, a.iters,
