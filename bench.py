@@ -377,6 +377,13 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
 
+    # stdout carries exactly one line, the JSON result: everything else the
+    # libraries print there (gloo's peer-connection notices, RCCL / HIP chatter)
+    # is sent to stderr, and the result is written to the saved stdout
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -528,7 +535,7 @@ def main():
             if world == 1 and not args.no_cpu_baseline and "c2_collision" in extra:
                 extra["c2_collision"]["cpu_baseline"] = cpu_baseline_collision(tg_np, solver.scene.to_json())
             out["extra"] = extra
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         dist.destroy_process_group()
     solver.close()
