@@ -24,7 +24,12 @@ The same JSON line carries, under `extra` (timed after the headline):
     (strong scaling), each step the shard solves plus the RCCL gather of q,
     flags and update counts to rank 0 (ikgrasp.parallel);
   * `c2_collision`: configs[1] with the reference's `success` (the collision
-    term of inverse_geometry.py:70, :97-98), with its own roofline and CPU leg.
+    term of inverse_geometry.py:70, :97-98), with its own roofline and CPU leg;
+  * `c2_yaw`: configs[1] with random cube yaw in [-pi/4, pi/4] (the "random
+    SE(3)" reading), with its own roofline and CPU leg.
+Every roofline block carries the executed-FP-ops fraction beside the
+SURVEY-count one, and a note wherever the SURVEY-count fraction exceeds 1.
+Multi-rank lines carry `ranks`: per-rank kernel ms and the gather's own ms.
 """
 import argparse
 import json
@@ -129,7 +134,7 @@ def cpu_baseline(targets, budget_s=10.0, numpy_budget_s=8.0):
         _, ok, _, _ = ik_oracle.computeqgrasppose(np.zeros(15), t[:9].reshape(3, 3), t[9:])
         nconv += bool(ok)
         k += 1
-    dn = time.perf_counter() - t0
+    dn = max(time.perf_counter() - t0, 1e-9)
     return {
         "value": value, "unit": "converged solves/s", "cores": threads, "kind": "port",
         "sample": f"{n} solves = the {len(targets)} benchmark targets x {n / len(targets):.2f}, q0=0, fp64 C "
@@ -139,7 +144,7 @@ def cpu_baseline(targets, budget_s=10.0, numpy_budget_s=8.0):
         "job_cpu_share": quota, "threads_used": threads,
         "per_thread_converged_per_s": value / threads,
         "all_physical_cores_extrapolated": (value / threads * physical) if physical else None,
-        "numpy_single_core": {
+        "numpy_single_core": None if k == 0 else {
             "value": nconv / dn, "unit": "converged solves/s", "cores": 1, "kind": "port",
             "sample": f"first {k} benchmark targets, oracle/ik_oracle.py (np.linalg.pinv per update), {dn:.1f} s, "
                       f"{nconv} converged; {k / dn:.2f} problems/s"},
@@ -220,7 +225,9 @@ def multistart_bytes(dtype, T, S, nq=15):
 
 def roofline(dtype, kernel, med, kern_ms, sum_iters, waves, simds, abytes, traffic, traffic_src):
     """The dominant kernel's VALU roofline (SURVEY count and executed count)
-    and its HBM figures (algorithmic bytes and counter bytes)."""
+    and its HBM figures (algorithmic bytes and counter bytes), for ONE GPU:
+    `sum_iters`, `waves`, `abytes` and `traffic` are that GPU's, `kern_ms` its
+    kernel time."""
     survey = (sum_iters * F_ITER) / (kern_ms * 1e-3) / 1e12 if sum_iters else None
     ex = flops_profile(kernel, dtype, med)
     executed = None
@@ -354,6 +361,41 @@ def reduce_stats(torch, dist, world, host, dev, vals, n_max):
     return t.tolist()
 
 
+def per_rank(torch, dist, world, host, dev, vals):
+    """Every rank's `vals` (a few floats) -> [world][len(vals)] on every rank."""
+    t = torch.tensor(vals, dtype=torch.float64, device="cpu" if host else dev)
+    if world == 1:
+        return [t.tolist()]
+    out = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]
+
+
+def time_collective(torch, dist, world, fn, reps=5):
+    """Mean wall ms of one blocking collective step `fn()`, each repetition
+    started from a barrier with the device idle and ended by a device
+    synchronize (untimed by the step loop: the diagnosable share of a step)."""
+    if world == 1:
+        return None
+    ms = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ms.append((time.perf_counter() - t0) * 1e3)
+    return float(np.mean(ms[1:]))
+
+
+def rank_block(per, world, backend, gather_ms, what):
+    """The per-rank figures of a multi-rank run (first diagnosis of an 8-GPU line)."""
+    km = [r[0] for r in per]
+    return {"world_size_seen": world, "backend": backend if world > 1 else None,
+            "kernel_ms_per_rank": km, "kernel_ms_min": min(km), "kernel_ms_max": max(km),
+            "gather_ms": gather_ms, "gather_is": what if world > 1 else "no collective at N=1"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -452,6 +494,14 @@ def main():
         gather.submit(qb)
 
     elapsed, kern_ms = timed(torch, dist, world, args.steps, args.warmup, step, stream, drain=gather.drain)
+    per = per_rank(torch, dist, world, host, dev, [kern_ms])
+
+    def gather_once():
+        if host:
+            dist.gather(q_out.cpu(), gathered, dst=0)
+        else:
+            dist.gather(q_out, gathered, dst=0)
+    gather_ms = time_collective(torch, dist, world, gather_once) if (world > 1 and not args.no_gather) else None
 
     n_conv = int(conv.sum().item())
     sum_iters = int(iters.to(torch.int64).sum().item())
@@ -528,6 +578,8 @@ def main():
             "mean_iters_all_problems": (tot_iters / (tot_B * S)) if S else None,
             "roofline": rl,
             "roofline_hbm": rl_hbm,
+            "ranks": rank_block(per, world, backend, gather_ms,
+                                f"blocking dist.gather of one step's q ({B}x15 {args.dtype}) to rank 0, wall ms"),
         }
         if world == 1 and not args.no_cpu_baseline and not S and not args.collision:
             out["cpu_baseline"] = cpu_baseline(tg_np)
@@ -559,6 +611,10 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
     i4 = torch.empty(n, dtype=torch.int32, device=dev)
     e4 = torch.empty((n, 2), dtype=torch.float64, device=dev)
 
+    def gather4():
+        for t in (q4, c4, i4):
+            gather_rows(t.cpu() if host else t, tot, dst=0)
+
     def step4(ev):
         if ev is not None:
             ev[0].record(stream)
@@ -566,16 +622,23 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            for t in (q4, c4, i4):
-                gather_rows(t.cpu() if host else t, tot, dst=0)
+            gather4()
 
     steps4 = max(3, min(args.steps, 5))
-    el4, km4 = timed(torch, dist, world, steps4, 1, step4, stream)
+    el4, km4_local = timed(torch, dist, world, steps4, 1, step4, stream)
+    it4_local = int(i4.to(torch.int64).sum().item())
+    per4 = per_rank(torch, dist, world, host, dev, [km4_local])
+    g4 = time_collective(torch, dist, world, gather4)
     el4, km4, conv4, it4 = reduce_stats(torch, dist, world, host, dev,
-                                        [el4, km4, int(c4.sum().item()), int(i4.to(torch.int64).sum().item())], 2)
+                                        [el4, km4_local, int(c4.sum().item()), it4_local], 2)
     del tg4, q4, c4, i4, e4
     if rank == 0:
         ps = el4 / steps4
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        # rank 0's shard, priced like the headline (one GPU's updates over its kernel time)
+        rl4, _ = roofline("f64", "pair", False, km4_local, it4_local, -(-n // 32), cus * 4,
+                          algorithmic_bytes("f64", n), None, None)
+        rl4["kernel"] = "ikg_pair_batch_kernel (rank 0's shard)"
         extra["c4_strong"] = {
             "workload": f"BASELINE configs[3]: {tot} targets (uniform_targets seed 7) split over {world} rank(s), "
                         "fp64, pair layout; each step the shard solves plus the gather of q, flags and update "
@@ -584,7 +647,10 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
             "value": conv4 / ps, "unit": "converged solves/s", "problems_per_s": tot / ps,
             "ms_per_step": ps * 1e3, "kernel_ms_max_rank": km4, "scaling": "strong", "n_gpus": world,
             "steps": steps4, "converged_fraction": conv4 / tot,
-            "roofline_survey_frac": it4 * F_ITER / (km4 * 1e-3) / 1e12 / PEAK_VALU["f64"] / world,
+            "roofline": rl4,
+            "ranks": rank_block(per4, world, "nccl" if not host else "gloo", g4,
+                                "blocking gather_rows of q, flags and update counts of the whole batch to rank 0, "
+                                "wall ms"),
         }
     # ---- C2 with the collision term (the reference's success)
     B = args.batch
@@ -623,6 +689,41 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
             "converged_fraction": convc / (B * world), "mean_iters": itc / (B * world),
             "roofline": rl, "roofline_hbm": rl_hbm,
         }
+    # ---- C2 with random yaw: the "random SE(3)" reading of configs[1] (the
+    # reference's "45 deg rotated" case, inverse_geometry_TESTS.py:266)
+    yaw = np.pi / 4
+    tgy_np = uniform_targets(B, seed=rank, yaw=yaw)
+    tgy = torch.tensor(tgy_np, dtype=torch.float64, device=dev)
+
+    def stepy(ev):
+        if ev is not None:
+            ev[0].record(stream)
+        solver.solve_into(tgy, q0, qc, cc, ic, ec, _lib.IKG_F64, sh)
+        if ev is not None:
+            ev[1].record(stream)
+
+    ely, kmy_local = timed(torch, dist, world, args.steps, args.warmup, stepy, stream)
+    ity_local = int(ic.to(torch.int64).sum().item())
+    ely, kmy, convy, ity = reduce_stats(torch, dist, world, host, dev,
+                                        [ely, kmy_local, int(cc.sum().item()), ity_local], 2)
+    if rank == 0:
+        ps = ely / args.steps
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        rl, rl_hbm = roofline("f64", "pair", False, kmy_local, ity_local, -(-B // 32), cus * 4,
+                              algorithmic_bytes("f64", B), None, None)
+        rl["kernel"] = "ikg_pair_batch_kernel"
+        extra["c2_yaw"] = {
+            "workload": f"BASELINE configs[1], random SE(3) reading: batch {B} per GPU, fp64, cube yaw ~ "
+                        f"U[-pi/4, pi/4] (inverse_geometry_TESTS.py:266 '45 deg rotated'), q0 = 0",
+            "value": convy / ps, "unit": "converged solves/s", "ms_per_step": ps * 1e3, "kernel_ms": kmy,
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "converged_fraction": convy / (B * world), "mean_iters": ity / (B * world),
+            "roofline": rl, "roofline_hbm": rl_hbm,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb = cpu_baseline(tgy_np, budget_s=6.0, numpy_budget_s=0.0)
+            cb.pop("numpy_single_core", None)
+            extra["c2_yaw"]["cpu_baseline"] = cb
     return extra
 
 

@@ -38,6 +38,33 @@ def solve(targets, q0, max_iters=1000, eps=1e-3, dt=1e-2, threads=0):
     return q_out, conv.astype(bool), iters, err
 
 
+# evaluation options of ikg_oracle_solve_ex (oracle/ikg_oracle.c, orc_opts)
+ACC_LOG6 = 1  # log3/log6 without the reference's acos((tr-1)/2) / 1-cos cancellation
+QR_STEP = 2   # pinv(J) e by Householder QR of J^T (np.linalg.pinv's error class)
+JITTER = 4    # every FK rotation entry moved by 0 / +-1 ulp: the reference's own rounding envelope
+
+
+def solve_ex(targets, q0, flags=0, seed=0, first=0, max_iters=1000, eps=1e-3, dt=1e-2, threads=0):
+    """`solve` with evaluation options (flags above; `seed` keys the jitter,
+    `first` is the problem index of row 0 so a subset reproduces a run)."""
+    lib = load()
+    f = lib.ikg_oracle_solve_ex
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int64, C.c_int, C.c_double, C.c_double, C.c_int,
+                  C.c_uint64, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    f.restype = C.c_int
+    tg = np.ascontiguousarray(targets, dtype=np.float64).reshape(-1, 12)
+    B = tg.shape[0]
+    q = np.ascontiguousarray(q0, dtype=np.float64)
+    stride = 0 if q.ndim == 1 else 15
+    q_out = np.empty((B, 15))
+    conv = np.empty(B, dtype=np.uint8)
+    iters = np.empty(B, dtype=np.int32)
+    err = np.empty((B, 2))
+    f(tg.ctypes.data, q.ctypes.data, stride, B, max_iters, eps, dt, flags, seed, first, q_out.ctypes.data,
+      conv.ctypes.data, iters.ctypes.data, err.ctypes.data, threads)
+    return q_out, conv.astype(bool), iters, err
+
+
 def has_collision():
     """The C restatement of the collision term (ikg_oracle_solve_collision) is built in."""
     return hasattr(load(), "ikg_oracle_solve_collision")

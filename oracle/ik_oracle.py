@@ -281,6 +281,115 @@ def computeqgrasppose(q0, cube_R, cube_t, max_iters=MAX_ITERS, dt=DT, eps=EPSILO
     return q, False, max_iters, (np.linalg.norm(eL), np.linalg.norm(eR))
 
 
+def computeqgrasppose_mp(q0, cube_R, cube_t, dps=32, max_iters=MAX_ITERS, dt=DT, eps=EPSILON):
+    """The loop of `computeqgrasppose` evaluated in `dps`-digit arithmetic
+    (mpmath) from the float64 model constants and inputs, rounded to float64
+    only at the end: the mathematically exact answer the float64 loops
+    approximate.  Where a trajectory is sensitive (random seeds, a slow
+    approach), the reference's own float64 result carries rounding noise of
+    ~1e-8 (its acos((tr-1)/2) near theta ~1e-3 loses ~10 digits), so this, not
+    one float64 run, is what "within 1e-9" is measured against
+    (tests/golden/sensitive_cases.npz).  Slow (~0.1 s per update)."""
+    import mpmath as mp
+    mp.mp.dps = dps
+    f = mp.mpf
+    pl = joint_placements()
+
+    def mat(A):
+        return [[f(float(A[i][j])) for j in range(3)] for i in range(3)]
+
+    def vec(v):
+        return [f(float(x)) for x in v]
+
+    def mm(A, B):
+        return [[A[i][0] * B[0][j] + A[i][1] * B[1][j] + A[i][2] * B[2][j] for j in range(3)] for i in range(3)]
+
+    def mv(A, v):
+        return [A[i][0] * v[0] + A[i][1] * v[1] + A[i][2] * v[2] for i in range(3)]
+
+    def mtv(A, v):
+        return [A[0][i] * v[0] + A[1][i] * v[1] + A[2][i] * v[2] for i in range(3)]
+
+    def tr(A):
+        return [[A[j][i] for j in range(3)] for i in range(3)]
+
+    def rot(axis, q):
+        s, c = mp.sin(q), mp.cos(q)
+        o, z = f(1), f(0)
+        if axis == 0:
+            return [[o, z, z], [z, c, -s], [z, s, c]]
+        if axis == 1:
+            return [[c, z, s], [z, o, z], [-s, z, c]]
+        return [[c, -s, z], [s, c, z], [z, z, o]]
+
+    def se3(A, B):
+        return (mm(A[0], B[0]), [A[1][i] + mv(A[0], B[1])[i] for i in range(3)])
+
+    P = [(mat(R0), vec(t0)) for R0, t0 in pl]
+    frames = [(j, mat(Rf), vec(tf)) for j, Rf, tf in (FRAME_LEFT, FRAME_RIGHT)]
+    cube = (mat(cube_R), vec(cube_t))
+    tgts = [se3(cube, (mat(H[0]), vec(H[1]))) for H in (HOOK_LEFT, HOOK_RIGHT)]
+    lo, hi = [f(float(x)) for x in LOWER], [f(float(x)) for x in UPPER]
+
+    def log6_mp(R, p):
+        sk = [R[2][1] - R[1][2], R[0][2] - R[2][0], R[1][0] - R[0][1]]
+        s = mp.sqrt(sk[0] ** 2 + sk[1] ** 2 + sk[2] ** 2) / 2
+        c = (R[0][0] + R[1][1] + R[2][2] - 1) / 2
+        th = mp.atan2(s, c)
+        if th >= mp.pi - f("1e-2"):
+            cphi = -c
+            b = th * th / (1 + cphi)
+            w = []
+            for i, (a_, b_) in enumerate(((2, 1), (0, 2), (1, 0))):
+                tmp = (R[i][i] + cphi) * b
+                sg = 1 if R[a_][b_] > R[b_][a_] else -1
+                w.append(sg * (mp.sqrt(tmp) if tmp > 0 else f(0)))
+        else:
+            k = th / (2 * s) if s > 0 else f("0.5")
+            w = [k * x for x in sk]
+        if th == 0:
+            al, be = f(1), f(1) / 12
+        else:
+            al = th * mp.sin(th) / (2 * (1 - mp.cos(th)))
+            be = 1 / (th * th) - mp.sin(th) / (2 * th * (1 - mp.cos(th)))
+        wp = w[0] * p[0] + w[1] * p[1] + w[2] * p[2]
+        cr = [w[1] * p[2] - w[2] * p[1], w[2] * p[0] - w[0] * p[2], w[0] * p[1] - w[1] * p[0]]
+        return [al * p[i] - cr[i] / 2 + be * wp * w[i] for i in range(3)] + w
+
+    q = [f(float(x)) for x in q0]
+    for it in range(max_iters + 1):
+        oMi = []
+        for j in range(NQ):
+            l = (mm(P[j][0], rot(AXIS[j], q[j])), P[j][1])
+            oMi.append(l if PARENT[j] < 0 else se3(oMi[PARENT[j]], l))
+        es, Js = [], []
+        for h, (j, Rf, tf) in enumerate(frames):
+            Rh, th_ = se3(oMi[j], (Rf, tf))
+            TR, Tt = tgts[h]
+            es.append(log6_mp(mm(tr(Rh), TR), mtv(Rh, [Tt[i] - th_[i] for i in range(3)])))
+            J = [[f(0)] * NQ for _ in range(6)]
+            i = j
+            while i >= 0:  # LOCAL: column = [R_f^T (a x (p_f - o_i)); R_f^T a]
+                a = [oMi[i][0][r][AXIS[i]] for r in range(3)]
+                d = [th_[r] - oMi[i][1][r] for r in range(3)]
+                cr = [a[1] * d[2] - a[2] * d[1], a[2] * d[0] - a[0] * d[2], a[0] * d[1] - a[1] * d[0]]
+                lin, ang = mtv(Rh, cr), mtv(Rh, a)
+                for r in range(3):
+                    J[r][i], J[3 + r][i] = lin[r], ang[r]
+                i = PARENT[i]
+            Js.append(J)
+        nL = mp.sqrt(sum(x * x for x in es[0]))
+        nR = mp.sqrt(sum(x * x for x in es[1]))
+        if it >= max_iters or (nL < eps and nR < eps):
+            break
+        Jm = mp.matrix(Js[0] + Js[1])
+        em = mp.matrix(es[0] + es[1])
+        x = Jm.T * mp.lu_solve(Jm * Jm.T, em)
+        q = [min(max(lo[k], q[k] + x[k] * f(dt)), hi[k]) for k in range(NQ)]
+    conv = bool(nL < eps and nR < eps) and it < max_iters
+    return np.array([float(v) for v in q]), conv, it, (float(nL), float(nR))
+
+
 def fk_hands(q):
     """(oMhandL, oMhandR) at q — used by tests for EE-space comparisons."""
     oMi = forward_kinematics(np.asarray(q, dtype=np.float64))

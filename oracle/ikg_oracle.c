@@ -48,6 +48,33 @@ typedef struct {
   double t[3];
 } se3;
 
+/* Evaluation options (test infrastructure, tests/test_c_oracle.py,
+ * tests/test_gpu_fullbatch.py).  0 = the reference's own formulas.
+ *   ORC_ACC_LOG6: log3/log6 evaluated without the cancellation of the
+ *     reference's acos((tr-1)/2) and 1-cos(theta) (theta = atan2(|skew|/2,
+ *     (tr-1)/2), alpha = theta(1+cos)/(2 sin)): the same mathematics,
+ *     rounded to ~1 ulp.  Near convergence (theta ~1e-3) the reference's theta
+ *     carries ~1e-13 absolute / 1e-10 relative rounding noise.
+ *   ORC_QR_STEP: the min-norm step pinv(J) e by Householder QR of J^T (error
+ *     ~eps cond(J), the class of np.linalg.pinv's SVD) instead of the normal
+ *     equations (~eps cond(J)^2).
+ *   ORC_JITTER: every entry of every FK rotation is moved by 0 or +-1 ulp
+ *     (a hash of jitter_seed, problem, update, joint, entry): the reference's
+ *     own rounding envelope (how far its output moves when its FK rounds
+ *     differently, as any other implementation's does). */
+enum { ORC_ACC_LOG6 = 1, ORC_QR_STEP = 2, ORC_JITTER = 4 };
+typedef struct {
+  int flags;
+  uint64_t seed; /* jitter: hash key, mixed with problem and update */
+} orc_opts;
+
+static uint64_t mix64(uint64_t x) {
+  x += 0x9e3779b97f4a7c15ull;
+  x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+  x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
 /* urdfdom rpy -> quaternion (normalised) -> Eigen matrix, yaw only */
 static void rpy_yaw(double yaw, double R[3][3]) {
   double z = sin(yaw / 2.0), w = cos(yaw / 2.0);
@@ -99,7 +126,7 @@ static void joint_local(int j, double q, se3* out) {
   if (j == 0) out->t[2] = ROBOT_Z + ORIGIN[0][2];
 }
 
-static void fk(const double* q, se3* oMi) {
+static void fk(const double* q, se3* oMi, const orc_opts* o, uint64_t key) {
   for (int j = 0; j < NQ; ++j) {
     se3 l;
     joint_local(j, q[j], &l);
@@ -107,6 +134,15 @@ static void fk(const double* q, se3* oMi) {
       oMi[j] = l;
     else
       mul(&oMi[PARENT[j]], &l, &oMi[j]);
+    if (o && (o->flags & ORC_JITTER)) {
+      uint64_t h = mix64(key ^ mix64((uint64_t)j + 0x51ull));
+      for (int k = 0; k < 9; ++k, h >>= 2) {
+        const int b = (int)(h & 3u); /* 0, 3: keep; 1: up; 2: down */
+        double* r = &oMi[j].R[k / 3][k % 3];
+        if (b == 1) *r = nextafter(*r, 2.0);
+        if (b == 2) *r = nextafter(*r, -2.0);
+      }
+    }
   }
 }
 
@@ -115,7 +151,13 @@ static void frame_placement_local(int h, se3* f) {
   for (int i = 0; i < 3; ++i) f->t[i] = FRAME_T[h][i];
 }
 
-static void log6(const se3* M, double e[6]) {
+static void log6_acc(const se3* M, double e[6]);
+
+static void log6(const se3* M, double e[6], int acc) {
+  if (acc) {
+    log6_acc(M, e);
+    return;
+  }
   const double pi = 3.14159265358979323846;
   const double (*R)[3] = M->R;
   double tr = R[0][0] + R[1][1] + R[2][2];
@@ -143,6 +185,47 @@ static void log6(const se3* M, double e[6]) {
     double st = sin(theta), ct = cos(theta);
     alpha = theta * st / (2.0 * (1.0 - ct));
     beta = 1.0 / t2 - st / (2.0 * theta * (1.0 - ct));
+  }
+  const double* p = M->t;
+  double wp = w[0] * p[0] + w[1] * p[1] + w[2] * p[2];
+  double cx = w[1] * p[2] - w[2] * p[1], cy = w[2] * p[0] - w[0] * p[2], cz = w[0] * p[1] - w[1] * p[0];
+  e[0] = alpha * p[0] - 0.5 * cx + beta * wp * w[0];
+  e[1] = alpha * p[1] - 0.5 * cy + beta * wp * w[1];
+  e[2] = alpha * p[2] - 0.5 * cz + beta * wp * w[2];
+  e[3] = w[0];
+  e[4] = w[1];
+  e[5] = w[2];
+}
+
+/* ORC_ACC_LOG6: the same log3/log6, every quantity from the rotation's skew
+ * part and trace without cancellation (the near-pi axis as the reference). */
+static void log6_acc(const se3* M, double e[6]) {
+  const double pi = 3.14159265358979323846;
+  const double (*R)[3] = M->R;
+  const double sk[3] = {R[2][1] - R[1][2], R[0][2] - R[2][0], R[1][0] - R[0][1]};
+  const double s = 0.5 * sqrt(sk[0] * sk[0] + sk[1] * sk[1] + sk[2] * sk[2]); /* sin theta */
+  const double c = 0.5 * (R[0][0] + R[1][1] + R[2][2] - 1.0);                 /* cos theta */
+  const double theta = atan2(s, c);
+  double w[3];
+  if (theta >= pi - 1e-2) {
+    double cphi = -c;
+    double beta = theta * theta / (1.0 + cphi);
+    double t0 = (R[0][0] + cphi) * beta, t1 = (R[1][1] + cphi) * beta, t2 = (R[2][2] + cphi) * beta;
+    w[0] = (R[2][1] > R[1][2] ? 1.0 : -1.0) * (t0 > 0 ? sqrt(t0) : 0.0);
+    w[1] = (R[0][2] > R[2][0] ? 1.0 : -1.0) * (t1 > 0 ? sqrt(t1) : 0.0);
+    w[2] = (R[1][0] > R[0][1] ? 1.0 : -1.0) * (t2 > 0 ? sqrt(t2) : 0.0);
+  } else {
+    const double t = s > 0.0 ? theta / (2.0 * s) : 0.5;
+    for (int i = 0; i < 3; ++i) w[i] = t * sk[i];
+  }
+  const double t2 = theta * theta;
+  double alpha, beta;
+  if (theta < 1e-2) { /* series: dropped terms < 1e-16 relative */
+    alpha = 1.0 - t2 / 12.0 - t2 * t2 / 720.0 - t2 * t2 * t2 / 30240.0;
+    beta = 1.0 / 12.0 + t2 / 720.0 + t2 * t2 / 30240.0 + t2 * t2 * t2 / 1209600.0;
+  } else {
+    alpha = theta < 0.5 * pi ? theta * (1.0 + c) / (2.0 * s) : theta * s / (2.0 * (1.0 - c));
+    beta = (1.0 - alpha) / t2;
   }
   const double* p = M->t;
   double wp = w[0] * p[0] + w[1] * p[1] + w[2] * p[2];
@@ -217,16 +300,60 @@ static int min_norm_step(double J[12][NQ], const double e[12], double dq[NQ]) {
   return 1;
 }
 
-static void hand_errors(const double* q, const se3 tgt[2], double e[12], double n[2]) {
+/* ORC_QR_STEP: x = pinv(J) e for full-row-rank J by Householder QR of
+ * A = J^T (NQ x 12): A = Q [R; 0], J = R^T Q^T, x = Q [R^-T e; 0]. */
+static int qr_step(double J[12][NQ], const double e[12], double dq[NQ]) {
+  double A[NQ][12], vs[12][NQ], beta[12];
+  for (int i = 0; i < NQ; ++i)
+    for (int j = 0; j < 12; ++j) A[i][j] = J[j][i];
+  for (int k = 0; k < 12; ++k) {
+    double nrm = 0.0;
+    for (int i = k; i < NQ; ++i) nrm += A[i][k] * A[i][k];
+    nrm = sqrt(nrm);
+    if (!(nrm > 0.0)) return 0;
+    const double alpha = A[k][k] > 0 ? -nrm : nrm;
+    double vn = 0.0;
+    for (int i = 0; i < NQ; ++i) vs[k][i] = i < k ? 0.0 : A[i][k];
+    vs[k][k] -= alpha;
+    for (int i = k; i < NQ; ++i) vn += vs[k][i] * vs[k][i];
+    beta[k] = vn > 0.0 ? 2.0 / vn : 0.0;
+    for (int j = k; j < 12; ++j) {
+      double d = 0.0;
+      for (int i = k; i < NQ; ++i) d += vs[k][i] * A[i][j];
+      d *= beta[k];
+      for (int i = k; i < NQ; ++i) A[i][j] -= d * vs[k][i];
+    }
+  }
+  /* R^T y = e (R = upper 12 x 12 of A) */
+  double x[NQ];
+  for (int i = 0; i < 12; ++i) {
+    double v = e[i];
+    for (int j = 0; j < i; ++j) v -= A[j][i] * x[j];
+    x[i] = v / A[i][i];
+  }
+  for (int i = 12; i < NQ; ++i) x[i] = 0.0;
+  /* x <- Q x = H_0 H_1 ... H_11 x */
+  for (int k = 11; k >= 0; --k) {
+    double d = 0.0;
+    for (int i = k; i < NQ; ++i) d += vs[k][i] * x[i];
+    d *= beta[k];
+    for (int i = k; i < NQ; ++i) x[i] -= d * vs[k][i];
+  }
+  for (int i = 0; i < NQ; ++i) dq[i] = x[i];
+  return 1;
+}
+
+static void hand_errors(const double* q, const se3 tgt[2], double e[12], double n[2], const orc_opts* o,
+                        uint64_t key) {
   se3 oMi[NQ];
-  fk(q, oMi);
+  fk(q, oMi, o, key);
   for (int h = 0; h < 2; ++h) {
     se3 f, oMf, hinv, M;
     frame_placement_local(h, &f);
     mul(&oMi[FRAME_JOINT[h]], &f, &oMf);
     inv(&oMf, &hinv);
     mul(&hinv, &tgt[h], &M);
-    log6(&M, e + 6 * h);
+    log6(&M, e + 6 * h, o && (o->flags & ORC_ACC_LOG6));
     double s = 0.0;
     for (int i = 0; i < 6; ++i) s += e[6 * h + i] * e[6 * h + i];
     n[h] = sqrt(s);
@@ -457,7 +584,7 @@ static int collide(const shape* a, const shape* b) {
 /* tools.collision (tools.py:25-35) at q with the cube target `cube` */
 static int collides(const col_scene* sc, const double* q, const se3* cube) {
   se3 oMi[NQ];
-  fk(q, oMi);
+  fk(q, oMi, NULL, 0);
   shape g[64];
   if (sc->n_geoms > 64) return -1;
   for (int k = 0; k < sc->n_geoms; ++k) {
@@ -483,7 +610,8 @@ static int collides(const col_scene* sc, const double* q, const se3* cube) {
 }
 
 static void solve_one(const double* target, const double* q0, int max_iters, double eps, double dt, double* q_out,
-                      uint8_t* conv, int32_t* iters, double* err, const col_scene* sc) {
+                      uint8_t* conv, int32_t* iters, double* err, const col_scene* sc, const orc_opts* o,
+                      int64_t problem) {
   se3 cube, hook, tgt[2];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) cube.R[i][j] = target[3 * i + j];
@@ -502,7 +630,7 @@ static void solve_one(const double* target, const double* q0, int max_iters, dou
   memcpy(q, q0, sizeof(q));
   int it = 0, ok = 0;
   for (;;) {
-    hand_errors(q, tgt, e, n);
+    hand_errors(q, tgt, e, n, o, o ? mix64(o->seed ^ mix64((uint64_t)problem)) ^ (uint64_t)it : 0);
     if (it >= max_iters) break;
     /* :70 -- errors pass and (with a scene) not collision(q) */
     if (n[0] < eps && n[1] < eps && !(sc && collides(sc, q, &cube))) {
@@ -510,9 +638,9 @@ static void solve_one(const double* target, const double* q0, int max_iters, dou
       break;
     }
     double J[12][NQ], dq[NQ];
-    frame_jacobian(q, 0, (double(*)[NQ])J[0]);
-    frame_jacobian(q, 1, (double(*)[NQ])J[6]);
-    if (!min_norm_step(J, e, dq)) break;
+    frame_jacobian(q, 0, J);
+    frame_jacobian(q, 1, J + 6);
+    if (!((o && (o->flags & ORC_QR_STEP)) ? qr_step(J, e, dq) : min_norm_step(J, e, dq))) break;
     for (int k = 0; k < NQ; ++k) {
       double v = q[k] + dq[k] * dt;
       v = v > LOWER[k] ? v : LOWER[k];
@@ -537,7 +665,23 @@ int ikg_oracle_solve(const double* targets, const double* q0, int64_t q0_stride,
 #endif
   for (int64_t i = 0; i < B; ++i)
     solve_one(targets + 12 * i, q0 + q0_stride * i, max_iters, eps, dt, q_out + NQ * i, conv + i, iters + i,
-              err + 2 * i, NULL);
+              err + 2 * i, NULL, NULL, i);
+  return 0;
+}
+
+/* ikg_oracle_solve with evaluation options (orc_opts above); `first` is the
+ * problem index of row 0 (the jitter hash key, so a subset reproduces a run). */
+int ikg_oracle_solve_ex(const double* targets, const double* q0, int64_t q0_stride, int64_t B, int max_iters,
+                        double eps, double dt, int flags, uint64_t seed, int64_t first, double* q_out, uint8_t* conv,
+                        int32_t* iters, double* err, int nthreads) {
+  const orc_opts o = {flags, seed};
+#ifdef _OPENMP
+  if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel for schedule(dynamic, 4)
+#endif
+  for (int64_t i = 0; i < B; ++i)
+    solve_one(targets + 12 * i, q0 + q0_stride * i, max_iters, eps, dt, q_out + NQ * i, conv + i, iters + i,
+              err + 2 * i, NULL, &o, first + i);
   return 0;
 }
 
@@ -556,7 +700,7 @@ int ikg_oracle_solve_collision(const double* targets, const double* q0, int64_t 
 #endif
   for (int64_t i = 0; i < B; ++i)
     solve_one(targets + 12 * i, q0 + q0_stride * i, max_iters, eps, dt, q_out + NQ * i, conv + i, iters + i,
-              err + 2 * i, &sc);
+              err + 2 * i, &sc, NULL, i);
   return 0;
 }
 

@@ -45,6 +45,17 @@
    oracle/generic_oracle.py (raw-axis Rodrigues restatement, itself checked
    against KAT-1/2 on the reference URDF here) from q = 0 and from perturbed
    q*, plus FK / LOCAL Jacobians / geometry placements at random q.
+10. `sensitive_cases.npz` — random-seed problems whose float64 trajectories
+   are the most sensitive to rounding (the largest distance between the C
+   restatement with the reference's log6 and with a cancellation-free log6,
+   over 4,096 (target, seed) pairs of the C5 workload plus target 390 / seed
+   231 of the round-3 C5 sample): inputs, the numpy oracle's answer (the
+   reference's step and log6), the answer of the same loop in 32-digit
+   arithmetic (ik_oracle.computeqgrasppose_mp: the mathematically exact loop),
+   and the reference's own rounding envelope (the C restatement with
+   np.linalg.pinv-class QR steps and every FK rotation entry moved by 0/+-1
+   ulp, 8 jitter seeds: the largest distance from the numpy answer, and
+   whether the update count / flag moved).
 """
 import json
 import os
@@ -183,6 +194,52 @@ def make_singular_cases():
     print("wrote singular_cases.npz:", n * 2, "cases; converged", sum(r[1] for r in res),
           "; numpy vs exact pinv |dq| max", float(dq.max()), "at cond0",
           float(np.array([r[10] for r in res])[dq.argmax()]))
+
+
+def _solve_mp(args):
+    target, q0 = args
+    q, ok, it, (nl, nr) = ik_oracle.computeqgrasppose_mp(q0, target[:9].reshape(3, 3), target[9:])
+    return q, ok, it, nl, nr
+
+
+def make_sensitive_cases(n_pool=4096, n_pick=9):
+    from oracle import c_oracle
+    m = load_nextage()
+    tg = uniform_targets(512, seed=41)
+    seeds = random_seeds(m, 256, seed=42)
+    seeds[0] = 0.0
+    rng = np.random.default_rng(44)
+    ti, si = rng.integers(0, 512, n_pool), rng.integers(0, 256, n_pool)
+    ti[0], si[0] = 390, 231  # the round-3 worst case (tests/test_gpu_configs.py)
+    T, Q = tg[ti], seeds[si]
+    qr, cr, ir, _ = c_oracle.solve_ex(T, Q, c_oracle.QR_STEP)
+    qa, ca, ia, _ = c_oracle.solve_ex(T, Q, c_oracle.ACC_LOG6 | c_oracle.QR_STEP)
+    dist = np.where(cr & ca & (ir == ia), np.abs(qr - qa).max(axis=1), 0.0)
+    flip = np.nonzero((cr != ca) | (ir != ia))[0]
+    pick = [0] + [int(i) for i in np.argsort(-dist) if i != 0][:n_pick - 1 - min(2, len(flip))] + \
+        [int(i) for i in flip[:2]]
+    T, Q = T[pick], Q[pick]
+    with Pool(8) as p:
+        ref = p.map(_solve, list(zip(T, Q)))
+        ex = p.map(_solve_mp, list(zip(T, Q)))
+    q_ref = np.array([r[0] for r in ref])
+    env, env_moves = np.zeros(len(pick)), np.zeros(len(pick), dtype=bool)
+    for s in range(1, 9):
+        qj, cj, ij, _ = c_oracle.solve_ex(T, Q, c_oracle.QR_STEP | c_oracle.JITTER, seed=s)
+        same = (cj == np.array([r[1] for r in ref])) & (ij == np.array([r[2] for r in ref]))
+        env = np.maximum(env, np.where(same, np.abs(qj - q_ref).max(axis=1), 0.0))
+        env_moves |= ~same
+    np.savez_compressed(
+        os.path.join(HERE, "sensitive_cases.npz"),
+        targets=T, q0=Q, target_index=ti[pick], seed_index=si[pick],
+        q=q_ref, converged=np.array([r[1] for r in ref]), iters=np.array([r[2] for r in ref], dtype=np.int32),
+        err=np.array([[r[3], r[4]] for r in ref]),
+        q_exact=np.array([r[0] for r in ex]), converged_exact=np.array([r[1] for r in ex]),
+        iters_exact=np.array([r[2] for r in ex], dtype=np.int32), err_exact=np.array([[r[3], r[4]] for r in ex]),
+        envelope=env, envelope_moves_flag=env_moves)
+    d = np.abs(q_ref - np.array([r[0] for r in ex])).max(axis=1)
+    print("wrote sensitive_cases.npz:", len(pick), "cases; numpy vs exact |dq|", np.array2string(d, precision=2),
+          "; envelope", np.array2string(env, precision=2), "; flag/count moves", env_moves.tolist())
 
 
 _SCENE = None
@@ -470,5 +527,7 @@ if __name__ == "__main__":
         make_control_cases()
     if "generic" in what:
         make_generic_cases()
+    if "sensitive" in what:
+        make_sensitive_cases()
     if "singular" in what:
         make_singular_cases()

@@ -83,3 +83,50 @@ def hands_from_tables(model, q):
         R, t = ik.se3_mul(oMi[int(model.arm_q[h][-1])], (model.hand_R[h], model.hand_t[h]))
         out.append(np.concatenate([R.reshape(9), t]))
     return np.array(out)
+
+
+def cpu_threads():
+    """CPUs this process may use: the affinity mask capped by a cgroup quota
+    (the GPU box gives a job 16 CPUs of a large host)."""
+    import os
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def rounding_envelope(targets, q0, q_ref, conv_ref, iters_ref, flags, runs=4, threads=0):
+    """How far the float64 loop's answer moves when its FK rounds differently:
+    the C oracle (oracle/ikg_oracle.c) with `flags` | JITTER (every FK rotation
+    entry moved by 0 / +-1 ulp) for `runs` jitter seeds.  Returns (env [B]:
+    the largest |q - q_ref| among runs with the same flag and update count,
+    outcomes [B]: the set of (converged, iters) the runs reached)."""
+    from oracle import c_oracle
+    B = len(targets)
+    env = np.zeros(B)
+    outcomes = [{(bool(conv_ref[i]), int(iters_ref[i]))} for i in range(B)]
+    for s in range(1, runs + 1):
+        q, c, it, _ = c_oracle.solve_ex(targets, q0, flags | c_oracle.JITTER, seed=s, threads=threads)
+        same = (c == conv_ref) & (it == iters_ref)
+        env = np.maximum(env, np.where(same, np.abs(q - q_ref).max(axis=1), 0.0))
+        for i in range(B):
+            outcomes[i].add((bool(c[i]), int(it[i])))
+    return env, outcomes
+
+
+def report(name, d):
+    """Print a comparison's counts and, with IKG_REPORT_DIR set, write them to
+    <dir>/<name>.json (profiles/r04/*_vs_oracle.json)."""
+    import json
+    import os
+    print(f"{name}: {json.dumps(d)}")
+    out = os.environ.get("IKG_REPORT_DIR")
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, f"{name}.json"), "w") as f:
+            json.dump(d, f, indent=1)

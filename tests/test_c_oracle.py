@@ -64,3 +64,41 @@ def test_collision_solve_without_pairs_is_plain_loop(scene):
     q2, c2, i2, _ = c_oracle.solve(d["targets"][:24], d["q0"][:24])
     assert (c1 == c2).all() and (i1 == i2).all()
     assert np.array_equal(q1, q2)
+
+
+# ---------------------------------------------------------------- evaluation modes
+def _kat_rows(kat):
+    return np.array([np.concatenate([np.array(kat[k]["R"]).reshape(9), kat[k]["t"]])
+                     for k in ("cube_placement", "cube_placement_target")])
+
+
+@pytest.mark.parametrize("flags", [0, c_oracle.ACC_LOG6, c_oracle.QR_STEP, c_oracle.ACC_LOG6 | c_oracle.QR_STEP,
+                                   c_oracle.QR_STEP | c_oracle.JITTER])
+def test_oracle_modes_reproduce_kats(kat, flags):
+    """Every evaluation mode is the same loop: KAT-1/2 (trajectory.json) in
+    740/736 updates.  These two trajectories are well conditioned, so even the
+    1-ulp FK jitter leaves q within a few ulp."""
+    q, conv, iters, _ = c_oracle.solve_ex(_kat_rows(kat), np.zeros(15), flags, seed=3)
+    assert conv.all() and iters.tolist() == [740, 736]
+    assert np.abs(q[0] - kat["q0"]).max() <= 1e-14 and np.abs(q[1] - kat["qe"]).max() <= 1e-14
+
+
+def test_sensitive_cases_rounding_envelope():
+    """tests/golden/sensitive_cases.npz: on rounding-sensitive random-seed
+    trajectories the reference's own float64 answer (numpy: pinv step,
+    Pinocchio's acos log6) is only defined up to its rounding envelope, and the
+    loop evaluated without log6's cancellation (C oracle ACC_LOG6 | QR_STEP)
+    lands at least as close to the 32-digit loop as the reference does."""
+    d = np.load(os.path.join(GOLD, "sensitive_cases.npz"))
+    assert np.array_equal(d["converged"], d["converged_exact"]) and np.array_equal(d["iters"], d["iters_exact"])
+    # the QR step with the reference's log6 reproduces numpy's answer within the envelope
+    q, c, it, _ = c_oracle.solve_ex(d["targets"], d["q0"], c_oracle.QR_STEP)
+    assert np.array_equal(c, d["converged"]) and np.array_equal(it, d["iters"])
+    assert (np.abs(q - d["q"]).max(axis=1) <= np.maximum(1e-9, 2 * d["envelope"])).all()
+    qa, ca, ia, _ = c_oracle.solve_ex(d["targets"], d["q0"], c_oracle.ACC_LOG6 | c_oracle.QR_STEP)
+    assert np.array_equal(ca, d["converged_exact"]) and np.array_equal(ia, d["iters_exact"])
+    ref = np.abs(d["q"] - d["q_exact"]).max(axis=1)
+    acc = np.abs(qa - d["q_exact"]).max(axis=1)
+    print("numpy vs exact", ref, "\nC acc vs exact", acc, "\nenvelope", d["envelope"])
+    assert (acc <= np.maximum(1e-9, ref + d["envelope"])).all()
+    assert ref.max() > 1e-8  # the fixture does hold cases where the reference's own answer is off by > 1e-8

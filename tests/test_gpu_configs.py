@@ -1,14 +1,13 @@
 """BASELINE.json configs at their stated sizes against the oracle (run on an MI355X).
 
-* C3 (65,536 targets, fp32): a seeded sample of 512 targets re-solved by the C
-  oracle (oracle/ikg_oracle.c, fp64, min-norm solve = pinv(J) e for full-rank J,
-  inverse_geometry.py:83); the mismatch counts the gates allow are printed and,
-  with IKG_REPORT_DIR set, written to <dir>/c3_vs_oracle.json.
+* C3 is compared in full (all 65,536) in tests/test_gpu_fullbatch.py.
 * C5 (multi-start, per-GPU share: 256 seeds x 512 targets), fp64 and both fp32
   layouts: the best seed equals the argmin over the expanded (target, seed)
   batch solve, and 64 targets re-solved by the oracle from their winning seed
-  agree (fp64: identical flags and update counts, q within 1e-9; fp32:
-  end-effector error <= 1e-4, counts within +-2).  The reference's analogue is
+  agree (fp64: q within 1e-9 of np.linalg.pinv's loop or within the
+  reference's own rounding envelope, see _c5_fp64_against_pinv; fp32:
+  end-effector error <= 1e-4, counts within +-2).  The full-size C5 (256 x
+  4,096 on one GPU) is in tests/test_gpu_fullbatch.py.  The reference's analogue is
   the resample-until-success loop of path.py:39-67.
 """
 import json
@@ -40,30 +39,6 @@ def _ee_err(solver, qa, qb):
     e = [helpers.se3_err(ha[:, h, :9].reshape(-1, 3, 3), ha[:, h, 9:], hb[:, h, :9].reshape(-1, 3, 3), hb[:, h, 9:])
          for h in range(2)]
     return np.maximum(e[0], e[1])
-
-
-def test_c3_sample_against_oracle(solver):
-    from ikgrasp.workload import uniform_targets
-    B = 65536
-    tg = uniform_targets(B, seed=1)
-    s32 = solver.solve(tg, np.zeros(15), dtype="f32")  # AUTO: the packed layout at this size
-    idx = np.sort(np.random.default_rng(31).choice(B, 512, replace=False))
-    q, conv, iters, _ = c_oracle.solve(tg[idx], np.zeros(15))
-    g_conv, g_it = s32.converged[idx], s32.iters[idx].astype(int)
-    both = conv & g_conv
-    flag_mis = int((conv != g_conv).sum())
-    it_off = np.abs(g_it[both] - iters[both])
-    ee = _ee_err(solver, q[both], s32.q[idx][both])
-    rep = dict(sample=512, oracle_converged=int(conv.sum()), gpu_converged=int(g_conv.sum()),
-               flag_mismatches=flag_mis, iters_outside_pm2=int((it_off > 2).sum()),
-               iters_max_abs_diff=int(it_off.max()) if it_off.size else 0,
-               ee_err_max=float(ee.max()) if ee.size else 0.0)
-    _report("c3_vs_oracle", rep)
-    # gates: SURVEY §8d C3 (EE <= 1e-4, counts +-2); a flag may flip only where the
-    # fp32 and fp64 error norms straddle eps within fp32 rounding
-    assert flag_mis <= 2
-    assert rep["iters_outside_pm2"] <= 2
-    assert rep["ee_err_max"] <= 1e-4
 
 
 @pytest.mark.parametrize("dtype,variant", [("f64", 0), ("f32", 1), ("f32", 2)])  # AUTO, PAIR, PACKED
@@ -105,54 +80,43 @@ def test_c5_share_multistart(solver, dtype, variant):
 
 
 def _c5_fp64_against_pinv(ms, tg, seeds, sel, rep):
-    """fp64 from random seeds, against the reference's own step (np.linalg.pinv,
-    inverse_geometry.py:83; oracle/ik_oracle.py), solved on the host's cores.
-    Random seeds start the loop in poorly scaled configurations (cond(J) up to
-    ~5e3 on this sample), so a 1e-16 rounding difference grows along the
-    trajectory: the C oracle's normal equations (cond^2) end 1.3e-8 from the
-    40-digit pinv (oracle.pinv_exact) where numpy's pinv ends 1.3e-9 from it.
-    The kernel's closed form (Sherman-Morrison over the arm blocks, a particular
-    solution projected off J's null vector) has the normal equations' error
-    class, not the SVD's.  Gates: flags and update counts identical except
-    where the stop test is a knife edge (the first run to stop passed it within
-    1e-7 of eps); q within 1e-9 of numpy's pinv on >= 90% of the sample; the
-    worst one no farther from the 40-digit pinv than 4x the C restatement
-    (normal equations) is from it."""
+    """fp64 from random seeds, against the reference's own step and log6
+    (np.linalg.pinv, Pinocchio's acos-based log3/log6; oracle/ik_oracle.py),
+    solved on the host's cores.  Random seeds start the loop in poorly scaled
+    configurations, and near convergence the reference's theta =
+    acos((tr-1)/2) loses ~10 digits (theta ~1e-3), so its own float64 answer
+    moves by up to ~1e-8 (some trajectories 1e-5) when its FK rounds one ulp
+    differently (tests/golden/sensitive_cases.npz pins this
+    against a 32-digit evaluation of the loop, which the kernel is closer to
+    than the reference is).  Gates: q within 1e-9 of numpy's answer, or within
+    twice the reference's rounding envelope (the C restatement with QR steps
+    and 1-ulp FK jitter, 6 runs); a flag / update-count difference must be an
+    outcome one of the jittered reference runs also reaches."""
     from concurrent.futures import ProcessPoolExecutor
     import multiprocessing as mpc
     args = [(seeds[ms.best_seed[j]].copy(), tg[j, :9].reshape(3, 3), tg[j, 9:]) for j in sel]
     with ProcessPoolExecutor(8, mp_context=mpc.get_context("spawn")) as ex:
         res = list(ex.map(o.computeqgrasppose, *zip(*args)))
-    eps = 1e-3
-    flips, dqs, worst = 0, [], None
-
-    def res_err(q, j):
-        eL, eR = o.hand_errors(q, *o.hook_targets(tg[j, :9].reshape(3, 3), tg[j, 9:]))
-        return np.linalg.norm(eL), np.linalg.norm(eR)
-    for (qp, okp, itp, _), j in zip(res, sel):
-        if okp != ms.converged[j] or itp != ms.iters[j]:
-            # the run that stopped first passed the test by a hair: its error
-            # at the stop is within rounding-growth of eps
-            flips += 1
-            early = float(ms.err[j].max()) if ms.iters[j] < itp else max(res_err(qp, j))
-            margin = eps - early
-            rep.setdefault("knife_edge_margins", []).append(margin)
-            assert 0 <= margin < 1e-7, (int(j), okp, itp, int(ms.iters[j]), margin)
-            continue
-        dq = float(np.abs(qp - ms.q[j]).max())
-        dqs.append(dq)
-        if worst is None or dq > worst[0]:
-            worst = (dq, j, qp)
-    rep.update(knife_edge_flips=flips, q_max_abs_diff_vs_pinv=max(dqs),
-               q_over_1e9=int((np.array(dqs) > 1e-9).sum()))
-    assert flips <= 1
-    assert rep["q_over_1e9"] <= len(sel) // 10, rep
-    dq, j, qp = worst
-    if dq > 1e-9:
-        sd = seeds[ms.best_seed[j]]
-        qx, okx, itx, _ = o.computeqgrasppose(sd.copy(), tg[j, :9].reshape(3, 3), tg[j, 9:], step=o.pinv_exact)
-        qc, _, _, _ = c_oracle.solve(tg[j][None], sd)
-        d_np, d_c, d_gpu = (float(np.abs(x - qx).max()) for x in (qp, qc[0], ms.q[j]))
-        rep.update(worst_target=int(j), worst_seed=int(ms.best_seed[j]), numpy_pinv_vs_exact=d_np,
-                   c_normal_eq_vs_exact=d_c, gpu_vs_exact=d_gpu)
-        assert d_gpu <= 4 * d_c + 1e-10, rep
+    qn = np.array([r[0] for r in res])
+    cn = np.array([r[1] for r in res])
+    itn = np.array([r[2] for r in res], dtype=np.int32)
+    same = (cn == ms.converged[sel]) & (itn == ms.iters[sel])
+    dq = np.where(same, np.abs(qn - ms.q[sel]).max(axis=1), 0.0)
+    check = np.nonzero(~same | (dq > 1e-9))[0]
+    bad = []
+    if len(check):
+        env, outc = helpers.rounding_envelope(tg[sel][check], seeds[ms.best_seed[sel]][check], qn[check], cn[check],
+                                              itn[check], c_oracle.QR_STEP, runs=6)
+        for k, i in enumerate(check):
+            j = sel[i]
+            got = (bool(ms.converged[j]), int(ms.iters[j]))
+            if got not in outc[k] or (same[i] and dq[i] > max(1e-9, 2 * env[k])):
+                bad.append(dict(target=int(j), seed=int(ms.best_seed[j]), gpu=got, numpy=[bool(cn[i]), int(itn[i])],
+                                dq=float(dq[i]), envelope=float(env[k]), jitter_outcomes=sorted(outc[k])))
+            else:
+                rep.setdefault("within_rounding_envelope", []).append(
+                    dict(target=int(j), seed=int(ms.best_seed[j]), dq=float(dq[i]), envelope=float(env[k]),
+                         outcome_differs=bool(not same[i])))
+    rep.update(outcome_differs=int((~same).sum()), q_max_abs_diff_vs_pinv=float(dq.max()),
+               q_over_1e9=int((dq > 1e-9).sum()), beyond_rounding_envelope=bad)
+    assert not bad, rep

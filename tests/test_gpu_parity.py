@@ -66,6 +66,26 @@ def test_fixture_parity_fp64(solver, oracle_cases):
         assert e.max() <= 1e-6
 
 
+def test_sensitive_cases_against_exact_loop(solver):
+    """Rounding-sensitive random-seed trajectories (tests/golden/
+    sensitive_cases.npz): flags and update counts equal the
+    32-digit evaluation of the loop; q within 1e-9 of it, or -- where no
+    float64 evaluation gets there (case 1: every float64 loop lands ~1e-5
+    away) -- no farther than the reference's own answer is plus the reference's
+    rounding envelope.  Printed: the kernel's and the reference's distances."""
+    import os
+    from conftest import GOLDEN
+    d = np.load(os.path.join(GOLDEN, "sensitive_cases.npz"))
+    for variant in (0, 3):  # AUTO (pair), QUAD
+        sol = solver.solve(d["targets"], d["q0"], variant=variant)
+        assert np.array_equal(sol.converged, d["converged_exact"]) and np.array_equal(sol.iters, d["iters_exact"])
+        gpu = np.abs(sol.q - d["q_exact"]).max(axis=1)
+        ref = np.abs(d["q"] - d["q_exact"]).max(axis=1)
+        print(f"variant {variant}: kernel vs exact", np.array2string(gpu, precision=2),
+              "\n  numpy reference vs exact", np.array2string(ref, precision=2))
+        assert (gpu <= np.maximum(1e-9, ref + d["envelope"])).all()
+
+
 def test_fixture_parity_fp32(solver, oracle_cases):
     c = oracle_cases
     sol = solver.solve(c["targets"], c["q0"], dtype="f32")
