@@ -1,0 +1,203 @@
+"""ikgrasp_binding.py -- the reference-side ctypes binding of the C-ABI
+(include/ikgrasp.h): what a maintainer adds next to the reference's
+inverse_geometry.py to run its IK loop (inverse_geometry.py:56-94) on the
+MI355X.  It reads the reference's own Pinocchio objects (RobotWrapper from
+setup_pinocchio.setuppinocchio, setup_pinocchio.py:73-83), so the tables come
+from the very model the reference uses, and imports the reference's `tools`
+and `config` modules.
+
+Checked by tests/test_binding.py: the structures' sizes and field offsets equal
+the C compiler's (a C probe of include/ikgrasp.h), and the descriptors built
+from a RobotWrapper-shaped robot equal the product's compiled tables, for
+Pinocchio 3 (Frame.parentJoint) and 2.x (Frame.parent); on an MI355X the
+drop-in reproduces KAT-1/2 (tests/test_gpu_bridge.py).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from config import EPSILON, LEFT_HAND, LEFT_HOOK, RIGHT_HAND, RIGHT_HOOK  # the reference's config.py:22-29
+from tools import setcubeplacement  # the reference's tools.py:62-68
+
+LIB = os.environ.get("IKGRASP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                     "motion-planning-and-control-for-dual-manipulator-robot_amd", "ikgrasp", "_native",
+                     "libikgrasp.so"))
+MAXNQ, ARM, MAXG, MAXP = 32, 6, 64, 1024
+
+
+class Desc(C.Structure):  # ikg_model_desc
+    _fields_ = [("nq", C.c_int32), ("parent", C.c_int32 * MAXNQ), ("axis", C.c_int32 * MAXNQ),
+                ("placement", (C.c_double * 12) * MAXNQ), ("lower", C.c_double * MAXNQ),
+                ("upper", C.c_double * MAXNQ), ("root_q", C.c_int32), ("arm_q", (C.c_int32 * ARM) * 2),
+                ("hand", (C.c_double * 12) * 2), ("hook", (C.c_double * 12) * 2)]
+
+
+class Params(C.Structure):  # ikg_params
+    _fields_ = [("eps", C.c_double), ("dt", C.c_double), ("max_iters", C.c_int32), ("variant", C.c_int32),
+                ("lam", C.c_double), ("problems_per_wave", C.c_int32), ("check_collision", C.c_int32)]
+
+
+class CDesc(C.Structure):  # ikg_collision_desc
+    _fields_ = [("n_geoms", C.c_int32), ("kind", C.c_int32 * MAXG), ("joint", C.c_int32 * MAXG),
+                ("placement", (C.c_double * 12) * MAXG), ("dims", (C.c_double * 3) * MAXG),
+                ("target_geom", C.c_int32), ("n_pairs", C.c_int32), ("pairs", (C.c_int32 * 2) * MAXP)]
+
+
+_vp = C.c_void_p
+
+
+class FKOut(C.Structure):  # ikg_frame_kin_out
+    _fields_ = [(n, _vp) for n in ("placement", "velocity", "J", "dJ", "dJv", "err", "derr")]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = C.CDLL(LIB)
+        L.ikg_model_create.argtypes = [C.POINTER(Desc), C.POINTER(_vp)]
+        L.ikg_model_destroy.argtypes = [_vp]
+        L.ikg_solve_batch.argtypes = [_vp, C.c_int, C.c_int, _vp, _vp, C.c_int64, C.c_int64, C.POINTER(Params),
+                                      _vp, _vp, _vp, _vp, _vp, C.c_uint32]
+        L.ikg_model_set_collision.argtypes = [_vp, C.POINTER(CDesc)]
+        L.ikg_distance_batch.argtypes = [_vp, C.c_int, C.c_int, _vp, _vp, C.c_int64, _vp, C.c_int32, _vp, _vp,
+                                         C.c_uint32]
+        L.ikg_frame_kinematics_batch.argtypes = [_vp, C.c_int, C.c_int, _vp, _vp, _vp, _vp, C.c_int64, C.c_int,
+                                                 C.POINTER(FKOut), _vp, C.c_uint32]
+        L.ikg_last_error.restype = C.c_char_p
+        _lib = L
+    return _lib
+
+
+_AXIS = {"JointModelRX": 0, "JointModelRY": 1, "JointModelRZ": 2}
+
+
+def _se3(M):
+    return list(np.asarray(M.rotation, dtype=np.float64).reshape(9)) + list(np.asarray(M.translation, dtype=np.float64))
+
+
+def _frame_joint(f):
+    """The frame's parent joint: Frame.parentJoint (Pinocchio 3.x; the 2.x
+    spelling Frame.parent is deprecated there, lab_0_geometry_with_pinocchio.ipynb:244)."""
+    j = getattr(f, "parentJoint", None)
+    return f.parent if j is None else j
+
+
+def _desc(robot, cube):
+    """robot.model (after translaterobot, setup_pinocchio.py:28-32) + the cube's hook frames -> ikg_model_desc."""
+    m, d = robot.model, Desc()
+    d.nq = m.nq                                   # Pinocchio joint j <-> q index j-1 (all 1-DoF revolute)
+    for j in range(1, m.njoints):
+        d.parent[j - 1] = m.parents[j] - 1
+        d.axis[j - 1] = _AXIS[m.joints[j].shortname()]
+        d.placement[j - 1][:] = _se3(m.jointPlacements[j])   # includes translaterobot (:32)
+        d.lower[j - 1], d.upper[j - 1] = m.lowerPositionLimit[j - 1], m.upperPositionLimit[j - 1]
+    chains = []
+    for h, name in enumerate((LEFT_HAND, RIGHT_HAND)):
+        f = next(fr for fr in m.frames if fr.name == name)    # model.getFrameId(name)
+        d.hand[h][:] = _se3(f.placement)
+        chain, j = [], _frame_joint(f)
+        while j > 0:
+            chain.append(j - 1)
+            j = m.parents[j]
+        chains.append(chain[::-1])
+    d.root_q = chains[0][0]
+    for a in range(2):
+        d.arm_q[a][:] = chains[a][1:]
+    for h, name in enumerate((LEFT_HOOK, RIGHT_HOOK)):
+        d.hook[h][:] = _se3(next(fr for fr in cube.model.frames if fr.name == name).placement)
+    return d
+
+
+def _shape(s):
+    """hpp-fcl shape -> (kind, dims); the cube mesh becomes its axis-aligned hull box."""
+    kind = type(s).__name__
+    if kind == "Sphere":
+        return 0, (s.radius, 0.0, 0.0)
+    if kind == "Box":
+        return 1, tuple(np.asarray(s.halfSide, dtype=np.float64))
+    if kind == "Cylinder":
+        return 2, (s.radius, s.halfLength, 0.0)
+    v = s.vertices() if callable(getattr(s, "vertices", None)) else s.vertices
+    v = np.asarray(v, dtype=np.float64).reshape(-1, 3)
+    return 3, tuple((v.max(0) - v.min(0)) / 2)
+
+
+def _cdesc(robot):
+    """robot.collision_model (after finalisecollisionsetup, setup_pinocchio.py:53-60) -> ikg_collision_desc."""
+    cm, d = robot.collision_model, CDesc()
+    d.n_geoms = len(cm.geometryObjects)
+    d.target_geom = d.n_geoms - 1                  # setcubeplacement moves geometryObjects[-1]
+    for g, go in enumerate(cm.geometryObjects):
+        d.joint[g] = go.parentJoint - 1            # universe -> -1
+        d.placement[g][:] = _se3(go.placement)     # includes translaterobot / loadobject placements
+        d.kind[g], d.dims[g][:] = _shape(go.geometry)
+    d.n_pairs = len(cm.collisionPairs)
+    for k, cp in enumerate(cm.collisionPairs):
+        d.pairs[k][:] = (cp.first, cp.second)
+    return d
+
+
+_model = None
+
+
+def _model_for(robot, cube):
+    global _model
+    if _model is None:
+        h = _vp()
+        rc = lib().ikg_model_create(C.byref(_desc(robot, cube)), C.byref(h))
+        if rc != 0:
+            raise RuntimeError(lib().ikg_last_error().decode())
+        rc = lib().ikg_model_set_collision(h, C.byref(_cdesc(robot)))
+        if rc != 0:
+            raise RuntimeError(lib().ikg_last_error().decode())
+        _model = h
+    return _model
+
+
+def computeqgrasppose(robot, qcurrent, cube, cubetarget, viz=None):
+    """Drop-in for inverse_geometry.computeqgrasppose (:17-100), collision term included."""
+    setcubeplacement(robot, cube, cubetarget)                      # :42
+    model = _model_for(robot, cube)
+    tgt = np.array(_se3(cubetarget), dtype=np.float64)
+    q0 = np.array(qcurrent, dtype=np.float64)                      # :49 copy
+    q = np.empty(robot.model.nq)
+    ok = np.zeros(1, np.uint8)
+    p = Params(EPSILON, 1e-2, 1000, 0, 0.0, 0, 1)                  # :53-54; 1 = collision term (:70, :97)
+    rc = lib().ikg_solve_batch(model, 0, 0, tgt.ctypes.data, q0.ctypes.data, 0, 1, C.byref(p),
+                               q.ctypes.data, ok.ctypes.data, None, None, None, 1)   # 1 = host pointers
+    if rc != 0:
+        raise RuntimeError(lib().ikg_last_error().decode())
+    return q, bool(ok[0])
+
+
+def distanceToObstacle(robot, q):
+    """tools.py:37-51 on the GPU (same pair selection)."""
+    cm = robot.collision_model
+    names = [g.name for g in cm.geometryObjects]
+    ids = (names.index("obstaclebase_0"), names.index("baseLink_0"))   # cm.getGeometryId
+    pairs = np.array([k for k, p in enumerate(cm.collisionPairs) if p.second in ids], dtype=np.int32)
+    q = np.asarray(q, dtype=np.float64)
+    tgt = np.array(_se3(cm.geometryObjects[-1].placement))
+    out = np.empty(1)
+    rc = lib().ikg_distance_batch(_model, 0, 0, q.ctypes.data, tgt.ctypes.data, 1, pairs.ctypes.data, len(pairs),
+                                  out.ctypes.data, None, 1)
+    if rc != 0:
+        raise RuntimeError(lib().ikg_last_error().decode())
+    return float(out[0])
+
+
+def task_space_terms(q, vq, q_des, vq_des):
+    """control.py:284-345 -> (J_total [12,15], J_dot_v_total [12], e [12], e_dot [12]) (LOCAL_WORLD_ALIGNED = 2)."""
+    f = lambda x: np.ascontiguousarray(x, dtype=np.float64)  # noqa: E731
+    q, vq, q_des, vq_des = f(q), f(vq), f(q_des), f(vq_des)
+    J, Jdv, e, ed = np.empty((12, 15)), np.empty(12), np.empty(12), np.empty(12)
+    out = FKOut(None, None, J.ctypes.data, None, Jdv.ctypes.data, e.ctypes.data, ed.ctypes.data)
+    rc = lib().ikg_frame_kinematics_batch(_model, 0, 0, q.ctypes.data, vq.ctypes.data, q_des.ctypes.data,
+                                          vq_des.ctypes.data, 1, 2, C.byref(out), None, 1)
+    if rc != 0:
+        raise RuntimeError(lib().ikg_last_error().decode())
+    return J, Jdv, e, ed

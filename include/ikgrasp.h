@@ -30,6 +30,18 @@
  *     the last failure on the calling thread is ikg_last_error().  Nothing
  *     throws or exits across this boundary.
  *   - Calls are re-entrant per (model, stream).
+ *
+ * Graphs
+ *   - Device-pointer solves are stream-ordered and may be captured into a
+ *     hipGraph (no host synchronisation, no blocking allocation).  Scratch a
+ *     captured solve needs (records, multi-start and continuation workspaces)
+ *     is allocated at capture time and owned by the captured graph (a graph
+ *     user object): it is released when the graph and all its executable
+ *     instantiations are destroyed, and freed by the model's next uncaptured
+ *     solve or by ikg_model_destroy.
+ *   - All instantiations of one captured graph share that scratch: do not
+ *     launch two of them concurrently (on different streams).
+ *   - Destroy graphs before the model: they also reference its device tables.
  */
 #ifndef IKGRASP_H
 #define IKGRASP_H

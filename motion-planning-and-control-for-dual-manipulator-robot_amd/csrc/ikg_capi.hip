@@ -239,6 +239,7 @@ template <typename T>
 int solve_batch_t(ikg_model* model, int device, const void* targets, const void* q0, int64_t q0_stride, int64_t B,
                   const ikg_params* params, void* q_out, uint8_t* converged, int32_t* iters, void* err_out,
                   hipStream_t s, uint32_t flags) {
+  if (!ikg::stream_capturing(s)) ikg::ws_drain(&model->ws);  // scratch of destroyed graphs
   const ikg::KModel<T>* dm = nullptr;
   int rc = model->device_tables<T>(device, &dm);
   if (rc) return rc;
@@ -330,6 +331,7 @@ template <typename T>
 int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_, const void* seeds, int64_t S,
                   const ikg_params* params, void* q_out, uint8_t* converged, int32_t* iters, void* err_out,
                   int32_t* best_seed, hipStream_t s, uint32_t flags) {
+  if (!ikg::stream_capturing(s)) ikg::ws_drain(&model->ws);  // scratch of destroyed graphs
   const ikg::KModel<T>* dm = nullptr;
   int rc = model->device_tables<T>(device, &dm);
   if (rc) return rc;
@@ -521,6 +523,17 @@ int ikg_log6_batch(int device, int dtype, const void* M, int64_t B, void* out, v
 
 const char* ikg_last_error(void) { return g_err; }
 
+// Diagnostic (not in include/ikgrasp.h): scratch buffers held by captured
+// graphs (live) and those whose graphs are gone, freed on the model's next
+// uncaptured solve (pending).  tests/test_gpu_graph.py.
+int ikg_debug_ws_count(const ikg_model* model, int64_t* live, int64_t* pending) {
+  if (!model || !live || !pending) return fail(IKG_EINVAL, "bad arguments");
+  std::lock_guard<std::mutex> lock(model->ws.st->mu);
+  *live = model->ws.st->live;
+  *pending = (int64_t)model->ws.st->pending.size();
+  return IKG_OK;
+}
+
 const char* ikg_version(void) { return "ikgrasp 0.1.0 (gfx950, pair kernel)"; }
 
 void ikg_params_default(ikg_params* p) {
@@ -587,12 +600,10 @@ void ikg_model_destroy(ikg_model* m) {
         ikg::jit_unload(*v[i]);
         delete v[i];
       }
-  // scratch held by captured graphs (the graphs must be gone by now: they
-  // also reference the model tables freed above)
-  for (auto& b : m->ws.bufs) {
-    (void)hipSetDevice(b.first);
-    (void)hipFree(b.second);
-  }
+  // scratch of captured graphs destroyed by now (a graph still alive keeps
+  // its buffer: graphs must be destroyed before the model, whose tables they
+  // also reference -- include/ikgrasp.h "Graphs")
+  ikg::ws_drain(&m->ws);
   if (prev >= 0) (void)hipSetDevice(prev);
   delete m;
 }

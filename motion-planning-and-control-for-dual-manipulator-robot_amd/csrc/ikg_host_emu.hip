@@ -18,6 +18,9 @@ namespace {
 thread_local long long lq_count = 0;
 thread_local long long jacobi_count = 0;  // arm solves of the LQ form that fell back to the Jacobi sweeps
 thread_local long long svd_count = 0;  // of those, with an arm that pins the chest (bb = 0: rank-deficient M_a)
+// updates whose two arm lanes computed different chest steps (must stay 0:
+// each lane carries the shared chest joint); ikg_emu_solve returns -3 then
+thread_local long long chest_mismatch = 0;
 
 // collide_wave's stages run serially (same functions, same order per lane).
 template <typename T>
@@ -145,7 +148,7 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
         minnorm_combine(z[arm][0], pv[arm][0], z[1 - arm][0], pv[1 - arm][0], sa[arm], f);
         for (int k = 0; k < 6; ++k) dqa[arm][k] = z[arm][1 + k] + f * pv[arm][1 + k];
       }
-      if (sa[0] != sa[1]) std::abort();  // both lanes must carry the same chest step
+      if (sa[0] != sa[1]) ++chest_mismatch;  // both lanes must carry the same chest step
       ++lq_count;
       if (pv[0][0] < T(Prec<T>::kRcond) || pv[1][0] < T(Prec<T>::kRcond)) ++svd_count;  // an arm pins s
     }
@@ -227,14 +230,17 @@ extern "C" long long ikg_emu_svd_count(int reset) {
 }
 
 // cd may be NULL; it is used when p->check_collision is set.
+// Returns 0, or -3 when the two lanes of a problem ever carried different
+// chest steps (a kernel invariant; the outputs are then not the kernel's).
 extern "C" int ikg_emu_solve(const ikg_model_desc* d, int dtype, const void* targets, const void* q0,
                              int64_t q0_stride, int64_t B, const ikg_params* p, void* q_out, uint8_t* conv,
                              int32_t* iters, void* err, void* trace, int trace_len, const ikg_collision_desc* cd) {
+  chest_mismatch = 0;
   if (dtype == IKG_F64)
     emu<double>(d, targets, q0, q0_stride, B, p, q_out, conv, iters, err, trace, trace_len, cd);
   else
     emu<float>(d, targets, q0, q0_stride, B, p, q_out, conv, iters, err, trace, trace_len, cd);
-  return 0;
+  return chest_mismatch ? -3 : 0;
 }
 
 template <typename T>

@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <memory>
 #include <mutex>
 #include <utility>
 #include <vector>
@@ -24,24 +25,74 @@ struct JitKernels;  // ikg_jit.hpp
 // used the default pool heavily (tests/test_gpu_graph.py with
 // IKG_TRAJ_REC=1; the same buffer from hipMalloc passed every replay).  So a
 // captured solve takes its scratch from hipMalloc (relaxed capture mode for
-// the call), owned by the model until ikg_model_destroy: a graph replays
-// with memory nobody else maps, and a graph never runs two replays at once.
-struct WsOwner {
+// the call) and hands it to the capturing graph as a user object
+// (hipGraphRetainUserObject): the buffer lives exactly as long as the graph
+// and its executable instantiations.  The user object's destructor may not
+// call HIP, so it only queues the buffer on the model's pending list; the
+// next uncaptured call into the library on that model (or
+// ikg_model_destroy) frees it.  Every instantiation of one captured graph
+// shares its scratch, so two of them must not run at the same time
+// (include/ikgrasp.h, "Graphs").
+struct WsState {
   std::mutex mu;
-  std::vector<std::pair<int, void*>> bufs;  // (device, pointer)
+  std::vector<std::pair<int, void*>> pending;  // (device, pointer) whose graphs are gone
+  int64_t live = 0;                            // buffers held by graphs
 };
+
+struct WsOwner {
+  std::shared_ptr<WsState> st = std::make_shared<WsState>();
+};
+
+struct GraphScratch {  // one captured buffer, owned by its graph's user object
+  std::shared_ptr<WsState> st;
+  int dev;
+  void* p;
+};
+
+inline void graph_scratch_release(void* arg) {  // user-object destructor: no HIP calls here
+  GraphScratch* g = static_cast<GraphScratch*>(arg);
+  {
+    std::lock_guard<std::mutex> lock(g->st->mu);
+    g->st->pending.emplace_back(g->dev, g->p);
+    --g->st->live;
+  }
+  delete g;
+}
 
 inline bool stream_capturing(hipStream_t s) {
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   return hipStreamIsCapturing(s, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
 }
 
+// Free the buffers of graphs destroyed since the last call (never while the
+// calling thread's stream is capturing: hipFree is not a capturable call).
+inline void ws_drain(WsOwner* owner) {
+  if (!owner) return;
+  std::vector<std::pair<int, void*>> v;
+  {
+    std::lock_guard<std::mutex> lock(owner->st->mu);
+    v.swap(owner->st->pending);
+  }
+  if (v.empty()) return;
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  for (auto& b : v) {
+    (void)hipSetDevice(b.first);
+    (void)hipFree(b.second);
+  }
+  if (prev >= 0) (void)hipSetDevice(prev);
+}
+
 inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s) {
   *p = nullptr;
   if (!owner || !stream_capturing(s)) return hipMallocAsync(p, bytes, s);
+  hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+  hipGraph_t graph = nullptr;
+  hipError_t e = hipStreamGetCaptureInfo_v2(s, &cst, nullptr, &graph, nullptr, nullptr);
+  if (e != hipSuccess || !graph) return e != hipSuccess ? e : hipErrorStreamCaptureInvalidated;
   hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
   (void)hipThreadExchangeStreamCaptureMode(&mode);
-  const hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+  e = hipMalloc(p, bytes ? bytes : 1);
   (void)hipThreadExchangeStreamCaptureMode(&mode);
   if (e != hipSuccess) {
     *p = nullptr;
@@ -49,12 +100,28 @@ inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s
   }
   int dev = 0;
   (void)hipGetDevice(&dev);
-  std::lock_guard<std::mutex> lock(owner->mu);
-  owner->bufs.emplace_back(dev, *p);
-  return hipSuccess;
+  GraphScratch* g = new GraphScratch{owner->st, dev, *p};
+  hipUserObject_t uo = nullptr;
+  e = hipUserObjectCreate(&uo, g, graph_scratch_release, 1, hipUserObjectNoDestructorSync);
+  if (e == hipSuccess) {
+    {
+      std::lock_guard<std::mutex> lock(owner->st->mu);
+      ++owner->st->live;
+    }
+    e = hipGraphRetainUserObject(graph, uo, 1, hipGraphUserObjectMove);  // the graph takes our reference
+    if (e != hipSuccess) (void)hipUserObjectRelease(uo, 1);                // -> destructor queues the buffer
+    return e;
+  }
+  delete g;
+  mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  (void)hipFree(*p);
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  *p = nullptr;
+  return e;
 }
 
-// the matching free: a captured solve's buffer stays with the owner
+// the matching free: a captured solve's buffer stays with its graph
 inline hipError_t ws_free(WsOwner* owner, void* p, hipStream_t s) {
   if (!p) return hipSuccess;
   if (owner && stream_capturing(s)) return hipSuccess;

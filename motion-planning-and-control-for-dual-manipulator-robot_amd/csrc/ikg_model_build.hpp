@@ -3,6 +3,7 @@
 #pragma once
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -27,6 +28,23 @@ inline bool is_identity(const double* R) {
     for (int c = 0; c < 3; ++c)
       if (R[3 * r + c] != (r == c ? 1.0 : 0.0)) return false;
   return true;
+}
+
+// A numeric test knob from the environment: parsed whole by strtod, finite and
+// >= 0, else ignored with a message; an accepted override is announced on
+// stderr (once per table build), so a stray value never changes results silently.
+template <typename T>
+inline void env_knob(const char* name, T& v) {
+  const char* e = std::getenv(name);
+  if (!e) return;
+  char* end = nullptr;
+  const double x = std::strtod(e, &end);
+  if (end == e || *end != '\0' || !std::isfinite(x) || x < 0) {
+    std::fprintf(stderr, "[ikgrasp] ignoring %s=\"%s\": not a finite number >= 0\n", name, e);
+    return;
+  }
+  std::fprintf(stderr, "[ikgrasp] test override %s=%g active\n", name, x);
+  v = (T)x;
 }
 
 template <typename T>
@@ -74,9 +92,10 @@ inline void build_kmodel(const ikg_model_desc& d, KModel<T>& k) {
   k.sing_tau = (T)(sizeof(T) == 8 ? IKG_SING_TAU64 : IKG_SING_TAU32);
   // test knobs, read when the tables are built: IKG_SING_BETA=0 (with
   // IKG_SING_TAU=1e30 for the generic path) sends every update through the
-  // LQ form
-  if (const char* e = std::getenv("IKG_SING_BETA")) k.sing_beta = (T)std::atof(e);
-  if (const char* e = std::getenv("IKG_SING_TAU")) k.sing_tau = (T)std::atof(e);
+  // LQ form.  A value must parse whole as a finite number >= 0; anything else
+  // is ignored with a message, and an accepted override is announced.
+  env_knob("IKG_SING_BETA", k.sing_beta);
+  env_knob("IKG_SING_TAU", k.sing_tau);
   bool used[IKG_MAX_NQ] = {};
   used[r] = true;
   for (int a = 0; a < 2; ++a)

@@ -6,7 +6,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "_build", "libikg_oracle.so")
+LIB = os.environ.get("IKG_ORACLE_LIB", os.path.join(HERE, "_build", "libikg_oracle.so"))
 _lib = None
 
 

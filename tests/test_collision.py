@@ -22,6 +22,8 @@ import json
 import os
 
 import numpy as np
+
+import helpers
 import pytest
 
 from conftest import GOLDEN
@@ -30,7 +32,7 @@ from ikgrasp.collision import load_nextage_scene
 from ikgrasp.model import load_nextage
 from oracle import collision_oracle as co
 
-EMU = os.path.join(os.path.dirname(_lib.LIB_PATH), "libikgrasp_emu.so")
+EMU = helpers.emu_path()
 
 
 @pytest.fixture(scope="module")
@@ -78,7 +80,7 @@ def emu():
         conv = np.empty(B, np.uint8)
         it = np.empty(B, np.int32)
         err = np.empty((B, 2), npt)
-        lib.ikg_emu_solve(C.byref(md), dtype, tg.ctypes.data, q0.ctypes.data, 15, B, C.byref(p), q.ctypes.data,
+        assert 0 == lib.ikg_emu_solve(C.byref(md), dtype, tg.ctypes.data, q0.ctypes.data, 15, B, C.byref(p), q.ctypes.data,
                           conv.ctypes.data, it.ctypes.data, err.ctypes.data, None, 0, C.byref(cd))
         return q, conv.astype(bool), it, err
 

@@ -7,6 +7,8 @@ import ctypes as C
 import os
 
 import numpy as np
+
+import helpers
 import pytest
 
 from ikgrasp import _lib
@@ -15,7 +17,7 @@ from oracle import collision_oracle as co
 
 @pytest.fixture(scope="module")
 def epa():
-    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libikgrasp_emu.so")
+    path = helpers.emu_path()
     if not os.path.exists(path):
         pytest.skip("libikgrasp_emu.so not built")
     lib = C.CDLL(path)

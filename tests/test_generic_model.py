@@ -9,6 +9,8 @@ import os
 import xml.etree.ElementTree as ET
 
 import numpy as np
+
+import helpers
 import pytest
 
 from conftest import GOLDEN
@@ -92,7 +94,7 @@ def test_emulated_kernel_solves_tilted_robot(model, gc, variant):
     specialisation -- the tilted robot's wrist joints meet in a point, so the
     decoupled wrist solve (SpecGenericWrist); 99: forced SpecGeneric, the 6x6
     Householder QR."""
-    emu = os.path.join(os.path.dirname(_lib.LIB_PATH), "libikgrasp_emu.so")
+    emu = helpers.emu_path()
     if not os.path.exists(emu):
         pytest.skip("libikgrasp_emu.so not built")
     lib = C.CDLL(emu)

@@ -198,3 +198,56 @@ def test_diag_collision_replays():
                   f"err {e[i].tolist()} / {e2[i].tolist()}")
     s.close()
     assert bad_total == 0
+
+
+def test_captured_scratch_lives_with_its_graph():
+    """a captured solve's scratch (records, workspaces) belongs to
+    the graph (a hipGraph user object), not to the model: it is held while the
+    graph lives, and freed on the model's next solve once the graph is
+    destroyed -- re-capturing does not accumulate buffers."""
+    import ctypes as C
+    import torch
+    from ikgrasp import _lib
+    from ikgrasp.collision import load_nextage_scene
+    from ikgrasp.solver import IKSolver
+    from ikgrasp.workload import uniform_targets
+    lib = _lib.load()
+    lib.ikg_debug_ws_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+
+    def counts(s):
+        live, pend = C.c_int64(), C.c_int64()
+        assert lib.ikg_debug_ws_count(s._h, C.byref(live), C.byref(pend)) == 0
+        return live.value, pend.value
+
+    dev = torch.device("cuda", 0)
+    s = IKSolver(device=0, scene=load_nextage_scene())
+    tg = torch.tensor(uniform_targets(512, seed=9), dtype=torch.float64, device=dev)
+    q0 = torch.zeros(15, dtype=torch.float64, device=dev)
+    out = _bufs(torch, 512, torch.float64, dev)
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        s.solve_into(tg, q0, *out, _lib.IKG_F64, side.cuda_stream, check_collision=True)
+    torch.cuda.synchronize()
+    assert counts(s) == (0, 0)
+    held = []
+    for k in range(3):  # re-capture three times
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            s.solve_into(tg, q0, *out, _lib.IKG_F64, torch.cuda.current_stream().cuda_stream, check_collision=True)
+        g.replay()
+        torch.cuda.synchronize()
+        live, pend = counts(s)
+        assert live >= 1
+        held.append(live)
+        g.reset()  # destroys the graph and its executable
+        import time
+        for _ in range(100):  # the user object's destructor may run after the destroy returns
+            torch.cuda.synchronize()
+            s.solve_into(tg, q0, *out, _lib.IKG_F64, torch.cuda.current_stream().cuda_stream, check_collision=True)
+            torch.cuda.synchronize()
+            if counts(s) == (0, 0):
+                break
+            time.sleep(0.02)
+        assert counts(s) == (0, 0), (k, counts(s))  # the destroyed graph's scratch was freed
+    assert held[0] == held[1] == held[2]
+    s.close()

@@ -7,12 +7,14 @@ import ctypes as C
 import os
 
 import numpy as np
+
+import helpers
 import pytest
 
 from ikgrasp import _lib
 from ikgrasp.model import load_nextage
 
-EMU = os.path.join(os.path.dirname(_lib.LIB_PATH), "libikgrasp_emu.so")
+EMU = helpers.emu_path()
 GENERIC = 99  # ikg_params.variant value the emulator reads as "force the generic path"
 
 
@@ -38,7 +40,7 @@ def emu():
         conv = np.empty(B, np.uint8)
         it = np.empty(B, np.int32)
         err = np.empty((B, 2), npt)
-        lib.ikg_emu_solve(C.byref(desc), dtype, tg.ctypes.data, q0.ctypes.data, stride, B, C.byref(p), q.ctypes.data,
+        assert 0 == lib.ikg_emu_solve(C.byref(desc), dtype, tg.ctypes.data, q0.ctypes.data, stride, B, C.byref(p), q.ctypes.data,
                           conv.ctypes.data, it.ctypes.data, err.ctypes.data, None, 0, None)
         return q, conv.astype(bool), it, err
 

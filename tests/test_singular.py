@@ -28,7 +28,7 @@ from conftest import GOLDEN
 from ikgrasp import _lib
 from ikgrasp.model import load_nextage
 
-EMU = os.path.join(os.path.dirname(_lib.LIB_PATH), "libikgrasp_emu.so")
+EMU = helpers.emu_path()
 
 
 @pytest.fixture(scope="module")
@@ -57,7 +57,7 @@ def emu():
         conv = np.empty(B, np.uint8)
         it = np.empty(B, np.int32)
         err = np.empty((B, 2), npt)
-        lib.ikg_emu_solve(C.byref(desc), dtype, tg.ctypes.data, q0.ctypes.data, 15, B, C.byref(p), q.ctypes.data,
+        assert 0 == lib.ikg_emu_solve(C.byref(desc), dtype, tg.ctypes.data, q0.ctypes.data, 15, B, C.byref(p), q.ctypes.data,
                           conv.ctypes.data, it.ctypes.data, err.ctypes.data, None, 0, None)
         return q, conv.astype(bool), it
 
