@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 3 evidence refresh: GPU tests, smoke, bench lines (C2 default with extras and CPU
+# Evidence refresh (round 3 on; RTAG names the output dir): GPU tests, smoke, bench lines (C2 default with extras and CPU
 # legs, C3, C4 share, C5 share, collision), rocprofv3 kernel-trace summaries, PMC passes.
 ROOT=$(pwd); O=$ROOT/gpurun_out/${RTAG:-refresh3}; mkdir -p $O; export TMPDIR=/tmp
 fatal() { case $1 in 0) return 0;; *) echo "FATAL $2 rc=$1" | tee -a $O/summary.txt; exit $1;; esac; }
