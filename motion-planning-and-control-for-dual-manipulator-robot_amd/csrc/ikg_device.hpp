@@ -1574,34 +1574,22 @@ struct ArmStateF1 {
   T e[6];      // pose error in frame-1 axes
 };
 
-// FK + pose error in frame 1 (inverse_geometry.py:58-67); returns |e|^2.
+// FK in frame 1 (the configuration-only half of arm_fk_error_f1): st.k,
+// st.o2, st.c12/s12, st.w, st.h and the hand rotation Rh.
 // sn/cs slots: 0 root, 1..6 arm joints 0..5.
 template <typename T, class SP>
-IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const T* sn, const T* cs,
-                                const T* RT, const T* tT, ArmStateF1<T>& st, ThetaTrack<T>* tk, bool resync) {
+IKG_HD inline void fk_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const T* sn, const T* cs,
+                         ArmStateF1<T>& st, T* R) {
   static_assert(kFrame1<SP>, "frame-1 path needs the Nextage joint pattern");
   const bool right = arm != 0;
-  // frame 1 = chest Rz(q_root) at root_t, then arm joint 0 at p_0 with Rz(q_0);
-  // trig slots as trig_exact_f1
-  const T sf = sn[0], cf = cs[0];
   T p0[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) p0[i] = SP::zero_t(0, i) ? T(0) : armc<T>(right, m->arm_t[0][0][i], m->arm_t[1][0][i]);
   st.k[0] = cs[1] * p0[0] + sn[1] * p0[1];
   st.k[1] = cs[1] * p0[1] - sn[1] * p0[0];
-  T RT1[9], tT1[3];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    RT1[c] = cf * RT[c] + sf * RT[3 + c];
-    RT1[3 + c] = cf * RT[3 + c] - sf * RT[c];
-    RT1[6 + c] = RT[6 + c];
-  }
-  const T d0 = tT[0] - m->root_t[0], d1 = tT[1] - m->root_t[1];
-  tT1[0] = cf * d0 + sf * d1 - st.k[0];
-  tT1[1] = cf * d1 - sf * d0 - st.k[1];
-  tT1[2] = tT[2] - m->root_t[2] - p0[2];
   // FK from arm joint 1 (R = I, origin of joint 0 at 0)
-  T R[9] = {T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1)};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0) ? T(1) : T(0);
   T t[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) t[i] = SP::zero_t(1, i) ? T(0) : armc<T>(right, m->arm_t[0][1][i], m->arm_t[1][1][i]);
@@ -1635,28 +1623,61 @@ IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__
   matvec3(R, ht, d);
 #pragma unroll
   for (int i = 0; i < 3; ++i) st.h[i] = t[i] + d[i];
+}
+
+// The pose error of frame-1 FK (the target-dependent half): the target moved
+// into frame 1 = chest Rz(q_root) at root_t, then arm joint 0 at p_0 with
+// Rz(q_0) (trig slots as trig_exact_f1), then log6 in the frame's axes;
+// st.e and the return value |e|^2.
+template <typename T, class SP>
+IKG_HD inline T pose_error_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const T* sn, const T* cs,
+                              const T* RT, const T* tT, ArmStateF1<T>& st, const T* R, ThetaTrack<T>* tk,
+                              bool resync) {
+  const bool right = arm != 0;
+  const T sf = sn[0], cf = cs[0];
+  const T p0z = SP::zero_t(0, 2) ? T(0) : armc<T>(right, m->arm_t[0][0][2], m->arm_t[1][0][2]);
+  T RT1[9], tT1[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    RT1[c] = cf * RT[c] + sf * RT[3 + c];
+    RT1[3 + c] = cf * RT[3 + c] - sf * RT[c];
+    RT1[6 + c] = RT[6 + c];
+  }
+  const T d0 = tT[0] - m->root_t[0], d1 = tT[1] - m->root_t[1];
+  tT1[0] = cf * d0 + sf * d1 - st.k[0];
+  tT1[1] = cf * d1 - sf * d0 - st.k[1];
+  tT1[2] = tT[2] - m->root_t[2] - p0z;
   pose_error_aligned(R, st.h, RT1, tT1, st.e, tk, resync);
   const T* e = st.e;
   return e[0] * e[0] + e[1] * e[1] + e[2] * e[2] + e[3] * e[3] + e[4] * e[4] + e[5] * e[5];
 }
 
+// FK + pose error in frame 1 (inverse_geometry.py:58-67); returns |e|^2.
+template <typename T, class SP>
+IKG_HD inline T arm_fk_error_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const T* sn, const T* cs,
+                                const T* RT, const T* tT, ArmStateF1<T>& st, ThetaTrack<T>* tk, bool resync) {
+  T R[9];
+  fk_f1<T, SP>(m, arm, sn, cs, st, R);
+  return pose_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, R, tk, resync);
+}
+
 // u = J_a^-1 e_a, v = J_a^-1 c_a in closed form (see above); alpha = u.v,
 // beta = v.v.  An exactly singular block gives a zero inverse, as in
-// inv3_apply2.
+// inv3_apply2.  Split in the configuration-only half (arm_solve_f1_v: the
+// inverses' scalars, v and beta) and the error half (arm_solve_f1_u: u and
+// alpha); the halves were split for a two-wave layout, measured slower.
+template <typename T>
+struct SolveF1V {
+  T iP0, iD, rH, c4r;  // 1/P0-type scalars of G^-1 and 1/c4 of H''^-1
+  T v[6];              // J_a^-1 c_a
+  T beta;              // |v|^2
+};
+
 template <typename T, class SP>
-IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
-                                const T* sn, const T* cs, T* u, T* v, T& alpha, T& beta) {
+IKG_HD inline void arm_solve_f1_v(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm,
+                                  const ArmStateF1<T>& st, const T* sn, const T* cs, SolveF1V<T>& sv) {
   const bool right = arm != 0;
   const T* w = st.w;
-  const T* ev = st.e;
-  const T* ew = st.e + 3;
-  // linear rows moved from the hand point to w
-  T wh[3], cr[3], bl[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) wh[i] = w[i] - st.h[i];
-  cross3(ew, wh, cr);
-#pragma unroll
-  for (int i = 0; i < 3; ++i) bl[i] = ev[i] + cr[i];
   // G: P0 = w, P1 = w - p_1, P2 = w - o_2
   T P1[3], P2[3];
 #pragma unroll
@@ -1669,45 +1690,82 @@ IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__
   // an exactly singular block gives inf / NaN here; the guard (pinv_step_f1,
   // on the bits of |v|^2) sends it to the per-arm pinv form
   const T rG = frcp(dG);
-  const T iP0 = det2 * rG, iD = w[0] * rG;
-  {
-    u[0] = bl[1] * iP0;
-    const T r0 = bl[0] + w[1] * u[0];
-    u[1] = -(P2[0] * r0 + P2[2] * bl[2]) * iD;
-    u[2] = (P1[2] * bl[2] + P1[0] * r0) * iD;
-  }
+  sv.iP0 = det2 * rG;
+  sv.iD = w[0] * rG;
+  T* v = sv.v;
   {  // root column at w: e_z x (w + (k, .)) = (-(w_y + k_y), w_x + k_x, 0)
-    v[0] = (w[0] + st.k[0]) * iP0;
+    v[0] = (w[0] + st.k[0]) * sv.iP0;
     const T r0 = w[1] * v[0] - (w[1] + st.k[1]);
-    v[1] = -P2[0] * r0 * iD;
-    v[2] = P1[0] * r0 * iD;
+    v[1] = -P2[0] * r0 * sv.iD;
+    v[2] = P1[0] * r0 * sv.iD;
   }
   // H = Ry(q12) H''; slots 4, 5 = arm joints 3, 4
   const T s3 = sn[4], c3 = cs[4], s4 = sn[5], c4 = cs[5];
-  const T rH = frcp(c4);
-  const T c4r = c4 * rH;
+  sv.rH = frcp(c4);
+  sv.c4r = c4 * sv.rH;
+  const T c12 = st.c12, s12 = st.s12;
+  {  // root column: z = Ry(q12)^T (e_z - (0, v1 + v2, v0))
+    const T z1 = -(v[1] + v[2]), z2 = T(1) - v[0];
+    const T y0 = -s12 * z2, y2 = c12 * z2;
+    v[5] = (c3 * y2 - s3 * z1) * sv.rH;
+    v[4] = (c3 * z1 + s3 * y2) * sv.c4r;
+    v[3] = y0 - s4 * v[5];
+  }
+  sv.beta = T(0);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) sv.beta += v[k] * v[k];
+}
+
+template <typename T, class SP>
+IKG_HD inline void arm_solve_f1_u(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm,
+                                  const ArmStateF1<T>& st, const T* sn, const T* cs, const SolveF1V<T>& sv, T* u,
+                                  T& alpha) {
+  const bool right = arm != 0;
+  const T* w = st.w;
+  const T* ev = st.e;
+  const T* ew = st.e + 3;
+  // linear rows moved from the hand point to w
+  T wh[3], cr[3], bl[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) wh[i] = w[i] - st.h[i];
+  cross3(ew, wh, cr);
+#pragma unroll
+  for (int i = 0; i < 3; ++i) bl[i] = ev[i] + cr[i];
+  T P1[3], P2[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    P1[i] = SP::zero_t(1, i) ? w[i] : w[i] - armc<T>(right, m->arm_t[0][1][i], m->arm_t[1][1][i]);
+    P2[i] = w[i] - st.o2[i];
+  }
+  {
+    u[0] = bl[1] * sv.iP0;
+    const T r0 = bl[0] + w[1] * u[0];
+    u[1] = -(P2[0] * r0 + P2[2] * bl[2]) * sv.iD;
+    u[2] = (P1[2] * bl[2] + P1[0] * r0) * sv.iD;
+  }
+  const T s3 = sn[4], c3 = cs[4], s4 = sn[5];
   const T c12 = st.c12, s12 = st.s12;
   {  // e: z = Ry(q12)^T (e_w - (0, x1 + x2, x0))
     const T z0 = ew[0], z1 = ew[1] - (u[1] + u[2]), z2 = ew[2] - u[0];
     const T y0 = c12 * z0 - s12 * z2, y2 = s12 * z0 + c12 * z2;
-    u[5] = (c3 * y2 - s3 * z1) * rH;
-    u[4] = (c3 * z1 + s3 * y2) * c4r;
+    u[5] = (c3 * y2 - s3 * z1) * sv.rH;
+    u[4] = (c3 * z1 + s3 * y2) * sv.c4r;
     u[3] = y0 - s4 * u[5];
   }
-  {  // root column: z = Ry(q12)^T (e_z - (0, v1 + v2, v0))
-    const T z1 = -(v[1] + v[2]), z2 = T(1) - v[0];
-    const T y0 = -s12 * z2, y2 = c12 * z2;
-    v[5] = (c3 * y2 - s3 * z1) * rH;
-    v[4] = (c3 * z1 + s3 * y2) * c4r;
-    v[3] = y0 - s4 * v[5];
-  }
   alpha = T(0);
-  beta = T(0);
 #pragma unroll
-  for (int k = 0; k < 6; ++k) {
-    alpha += u[k] * v[k];
-    beta += v[k] * v[k];
-  }
+  for (int k = 0; k < 6; ++k) alpha += u[k] * sv.v[k];
+}
+
+template <typename T, class SP>
+IKG_HD inline void arm_solve_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
+                                const T* sn, const T* cs, T* u, T* v, T& alpha, T& beta) {
+  SolveF1V<T> sv;
+  arm_solve_f1_v<T, SP>(m, arm, st, sn, cs, sv);
+  arm_solve_f1_u<T, SP>(m, arm, st, sn, cs, sv, u, alpha);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) v[k] = sv.v[k];
+  beta = sv.beta;
 }
 
 // The guard's test: x beyond the bound, or inf / NaN (compared as unsigned
