@@ -233,6 +233,10 @@ static bool rec_in_batch() {
   return !(e && atoi(e) == 0);
 }
 constexpr size_t kRecBudget = size_t(1) << 30;
+static size_t rec_budget() {  // IKG_REC_BUDGET_MB: measurement knob
+  const char* e = getenv("IKG_REC_BUDGET_MB");
+  return e ? (size_t)atoll(e) << 20 : kRecBudget;
+}
 
 
 template <typename T>
@@ -286,7 +290,7 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
       rec_in_batch()) {
     const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
     const size_t b_rec = (sizeof(T) * rl * ((size_t)params->max_iters + 1) * (size_t)B + 255) & ~(size_t)255;
-    if (b_rec <= kRecBudget && ikg::ws_alloc(&model->ws, &rec, b_rec + sizeof(int32_t) * (size_t)B, s) == hipSuccess) {
+    if (b_rec <= rec_budget() && ikg::ws_alloc(&model->ws, &rec, b_rec + sizeof(int32_t) * (size_t)B, s) == hipSuccess) {
       a.rec = rec;
       a.rec_n = (int32_t*)((char*)rec + b_rec);
       ikg::ws_trace("alloc rec", rec, b_rec + sizeof(int32_t) * (size_t)B, s);

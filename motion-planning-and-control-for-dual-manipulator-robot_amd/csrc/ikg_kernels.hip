@@ -213,6 +213,8 @@ template <typename T, bool DAMPED, class SP>
 static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
   const int ppw = a.ppw;
   const dim3 grid((unsigned)((a.B + ppw - 1) / ppw));
+  // IKG_FORCE_MED=1: measurement knob, the medium-range series for every launch
+  static const bool force_med = getenv("IKG_FORCE_MED") && atoi(getenv("IKG_FORCE_MED")) != 0;
   // per-problem seeds (multi-start, or a q0 row per target): large first steps
   // are common, so the frame-1 loop takes the medium-range trig series
   if constexpr (kFrame1<SP> && !DAMPED) {
@@ -223,7 +225,7 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
       if (a.rec_used) *a.rec_used = true;
       return;
     }
-    if (a.S > 1 || a.q0_stride != 0) {
+    if (a.S > 1 || a.q0_stride != 0 || force_med) {
       hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, true>), grid, dim3(64), lds_pad_bytes(), s, dmodel,
                          prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out,
                          a.converged, a.iters, (T*)a.err_out);
@@ -292,7 +294,9 @@ hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, con
     if (a.variant == IKG_VARIANT_QUAD) return hipErrorInvalidValue;  // checked by the C-ABI first
   }
   if constexpr (std::is_same<T, float>::value) {
-    const bool want = a.variant == IKG_VARIANT_PACKED || (a.variant == IKG_VARIANT_AUTO && a.B >= packed_min_batch());
+    static const bool rec_pair = getenv("IKG_REC_PREFER_PAIR") && atoi(getenv("IKG_REC_PREFER_PAIR")) != 0;
+    const bool want = a.variant == IKG_VARIANT_PACKED ||
+                      (a.variant == IKG_VARIANT_AUTO && a.B >= packed_min_batch() && !(rec_pair && a.rec));
     if (want && packed_applies(prm, spec)) {
       return launch_packed_batch(dmodel, prm, a, s);
     }

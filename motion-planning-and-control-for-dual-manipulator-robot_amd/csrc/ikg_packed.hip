@@ -133,7 +133,8 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
                        (float*)a.err_out);
   };
   // per-problem seeds: the medium-range trig series (ikg_device.hpp trig_advance_f1)
-  const bool med = a.S > 1 || a.q0_stride != 0;
+  static const bool force_med = getenv("IKG_FORCE_MED") && atoi(getenv("IKG_FORCE_MED")) != 0;  // measurement knob
+  const bool med = a.S > 1 || a.q0_stride != 0 || force_med;
   if (need == 1 && capped_ok<1>())
     med ? go(ikg_packed_batch_kernel<SpecNextage, 1, true>) : go(ikg_packed_batch_kernel<SpecNextage, 1, false>);
   else if (need == 2 && capped_ok<2>())
