@@ -30,6 +30,16 @@
  *     the last failure on the calling thread is ikg_last_error().  Nothing
  *     throws or exits across this boundary.
  *   - Calls are re-entrant per (model, stream).
+ *   - Results are deterministic.  A problem's fp64 answer is the same bit for
+ *     bit in any batch size, batch position and collision schedule, with
+ *     one exception: a broadcast q0 (q0_stride = 0) and per-problem q0 rows
+ *     (and multi-start seeds) advance the joint sin/cos by different rules for
+ *     steps of 0.025..0.25 rad (exact sincos / a longer series), so when such
+ *     steps occur -- random seeds, not the reference's q0 = 0 on its sampler's
+ *     targets -- the two agree to rounding (<= 1e-10 over 150 updates), not
+ *     bit for bit.  A multi-start's seed equals a per-row solve of that seed
+ *     bit for bit.  fp32 results also depend on the kernel layout (PAIR /
+ *     PACKED), which AUTO picks by batch size.
  *
  * Graphs
  *   - Device-pointer solves are stream-ordered and may be captured into a

@@ -239,6 +239,28 @@ static size_t rec_budget() {  // IKG_REC_BUDGET_MB: measurement knob
 }
 
 
+// Records of the collision continuation for `n` problems (see solve_batch_t),
+// or null when they exceed the budget (the continuation then recomputes the
+// iterates past the first passing one: the trajectory kernel).
+template <typename T>
+void* offer_records(ikg_model* model, ikg::BatchArgs& a, const ikg_params& params, int64_t n, int nq, hipStream_t s,
+                    bool* rec_used) {
+  const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
+  const size_t b_rec = (sizeof(T) * rl * ((size_t)params.max_iters + 1) * (size_t)n + 255) & ~(size_t)255;
+  void* rec = nullptr;
+  if (b_rec > rec_budget() || ikg::ws_alloc(&model->ws, &rec, b_rec + sizeof(int32_t) * (size_t)n, s) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  a.rec = rec;
+  a.rec_n = (int32_t*)((char*)rec + b_rec);
+  ikg::ws_trace("alloc rec", rec, b_rec + sizeof(int32_t) * (size_t)n, s);
+  ikg::poison_float(rec, b_rec, s);
+  ikg::poison_int(a.rec_n, sizeof(int32_t) * (size_t)n, s);
+  a.rec_used = rec_used;
+  return rec;
+}
+
 template <typename T>
 int solve_batch_t(ikg_model* model, int device, const void* targets, const void* q0, int64_t q0_stride, int64_t B,
                   const ikg_params* params, void* q_out, uint8_t* converged, int32_t* iters, void* err_out,
@@ -282,26 +304,12 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   a.jit = model->jit_kernels<T>(device);
   // collision term, pair layout, Nextage loop: the batch kernel itself records
   // every iterate from the first passing one on, for the continuation's scan
-  // (ikg_collision.hip); the records take (max_iters + 1) x
-  // rec_len values per problem, offered up to kRecBudget
+  // (ikg_collision.hip), whatever the q0 layout; the records
+  // take (max_iters + 1) x rec_len values per problem, offered up to the budget
   bool rec_used = false;
   void* rec = nullptr;
-  if (dc && model->spec == ikg::kSpecNextage && !(params->lambda > 0) && !a.jit && a.q0_stride == 0 &&
-      rec_in_batch()) {
-    const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
-    const size_t b_rec = (sizeof(T) * rl * ((size_t)params->max_iters + 1) * (size_t)B + 255) & ~(size_t)255;
-    if (b_rec <= rec_budget() && ikg::ws_alloc(&model->ws, &rec, b_rec + sizeof(int32_t) * (size_t)B, s) == hipSuccess) {
-      a.rec = rec;
-      a.rec_n = (int32_t*)((char*)rec + b_rec);
-      ikg::ws_trace("alloc rec", rec, b_rec + sizeof(int32_t) * (size_t)B, s);
-      ikg::poison_float(rec, b_rec, s);
-      ikg::poison_int(a.rec_n, sizeof(int32_t) * (size_t)B, s);
-      a.rec_used = &rec_used;
-    } else {
-      rec = nullptr;
-      (void)hipGetLastError();
-    }
-  }
+  if (dc && model->spec == ikg::kSpecNextage && !(params->lambda > 0) && !a.jit && rec_in_batch())
+    rec = offer_records<T>(model, a, *params, B, nq, s, &rec_used);
   hipError_t e = ikg::launch_pair_batch<T>(dm, kparams<T>(params), a, model->spec, s);
   if (e != hipSuccess) {
     if (rec) {
@@ -382,7 +390,23 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   a.ws_err = ws + b_q;
   a.ws_iters = (int32_t*)(ws + b_q + b_err);
   a.ws_conv = (uint8_t*)(ws + b_q + b_err + b_it);
+  // the collision continuation's records, as solve_batch_t (same values for a
+  // seed whatever call solves it)
+  bool rec_used = false;
+  void* rec = nullptr;
+  if (a.collision && model->spec == ikg::kSpecNextage && !(params->lambda > 0) && !a.jit && rec_in_batch()) {
+    ikg::BatchArgs tmp{};
+    rec = offer_records<T>(model, tmp, *params, n, nq, s, &rec_used);
+    a.rec = tmp.rec;
+    a.rec_n = tmp.rec_n;
+    a.rec_used = tmp.rec_used;
+  }
   e = ikg::launch_multistart<T>(dm, kparams<T>(params), a, model->spec, s);
+  if (rec) {
+    ikg::ws_trace("free rec", rec, 0, s);
+    const hipError_t ef = ikg::ws_free(&model->ws, rec, s);
+    if (e == hipSuccess) e = ef;
+  }
   ikg::ws_trace("free multistart", ws, 0, s);
   hipError_t e2 = ikg::ws_free(&model->ws, ws, s);
   if (e != hipSuccess) return hip_fail(e, "ikg multistart kernel launch");

@@ -1331,12 +1331,40 @@ IKG_HD inline void trig_exact_f1(const KModel<typename LaneT<T>::E>* __restrict_
   add_angles(s[6], c[6], hs, hc, sn[6], cs[6]);
 }
 
-// MED: steps beyond the short series' range take a longer series (kIncMed)
-// before falling back to the exact sincos of every slot.  It pays where such
-// steps are common (per-problem seeds: random-seed batches 6.46 -> 5.06 ms fp64,
-// 3.08 -> 2.73 ms fp32 at 131,072) and costs ~5% where they are rare (C2 from
-// q = 0: 0.99 -> 1.04 ms, the extra branch's register pressure), so the
-// launchers pick it per launch (ikg_kernels.hip, ikg_packed.hip).
+// One trig advance with the medium-range rule, per lane: the short series for
+// steps within kIncMax, the longer series (kIncMed) for steps up to kIncMed,
+// the exact sincos beyond that and at resyncs.
+template <typename T>
+IKG_HD inline void trig_med_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, T qc, const T* qa,
+                               const T* d, bool resync, T* sn, T* cs) {
+  T dmax = fabs(d[0]);
+#pragma unroll
+  for (int j = 1; j < 7; ++j) dmax = fmax(dmax, fabs(d[j]));
+  if (resync || any_of(dmax > T(Trig<T>::kIncMax))) {
+    // steps beyond the short series' range: first steps from random seeds
+    // (multi-start took this path on 14% of its fp64 updates); a longer series
+    // covers them up to kIncMed, the exact sincos beyond and at resyncs
+    if (!resync && all_of(mnot(dmax > T(Trig<T>::kIncMed)))) {
+#pragma unroll
+      for (int j = 0; j < 7; ++j) Trig<T>::step_med(d[j], sn[j], cs[j]);
+    } else {
+      trig_exact_f1(m, arm, qc, qa, sn, cs);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
+  }
+}
+
+// MED = true: the medium-range rule (per-problem seeds: large first steps are
+// common; random-seed batches 6.46 -> 5.06 ms fp64, 3.08 -> 2.73 ms fp32 at
+// 131,072 against the exact fallback).  MED = false (a broadcast q0): the short
+// series runs in place and a lane whose step leaves its range (or a resync)
+// takes the exact sincos of every slot, in a wave-uniform branch.  The two
+// rules differ only on steps of 0.025..0.25 rad, by rounding (C2 from q = 0 has
+// none); the medium-range rule inline costs the broadcast kernel 4% fp64 /
+// 3.5% fp32 at C2, and the out-of-line form with it 21 register copies per
+// update (profiles/r04/trig/).
 template <typename T, bool MED = false>
 IKG_HD inline void trig_advance_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, T qc, const T* qa,
                                    const T* q_old, bool resync, T* sn, T* cs) {
@@ -1370,23 +1398,7 @@ IKG_HD inline void trig_advance_f1(const KModel<typename LaneT<T>::E>* __restric
     }
     return;
   }
-  T dmax = fabs(d[0]);
-#pragma unroll
-  for (int j = 1; j < 7; ++j) dmax = fmax(dmax, fabs(d[j]));
-  if (resync || any_of(dmax > T(Trig<T>::kIncMax))) {
-    // steps beyond the short series' range: first steps from random seeds
-    // (multi-start took this path on 14% of its fp64 updates); a longer series
-    // covers them up to kIncMed, the exact sincos beyond and at resyncs
-    if (!resync && all_of(mnot(dmax > T(Trig<T>::kIncMed)))) {
-#pragma unroll
-      for (int j = 0; j < 7; ++j) Trig<T>::step_med(d[j], sn[j], cs[j]);
-    } else {
-      trig_exact_f1(m, arm, qc, qa, sn, cs);
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
-  }
+  trig_med_f1(m, arm, qc, qa, d, resync, sn, cs);
 }
 
 // FK + pose error; returns |e|^2 (inverse_geometry.py:58-67; the stop test

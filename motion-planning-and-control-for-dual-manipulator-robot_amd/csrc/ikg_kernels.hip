@@ -213,19 +213,26 @@ template <typename T, bool DAMPED, class SP>
 static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
   const int ppw = a.ppw;
   const dim3 grid((unsigned)((a.B + ppw - 1) / ppw));
-  // IKG_FORCE_MED=1: measurement knob, the medium-range series for every launch
+  // IKG_FORCE_MED=1: measurement knob, the inline medium-range rule for every launch
   static const bool force_med = getenv("IKG_FORCE_MED") && atoi(getenv("IKG_FORCE_MED")) != 0;
   // per-problem seeds (multi-start, or a q0 row per target): large first steps
-  // are common, so the frame-1 loop takes the medium-range trig series
+  // are common, so the frame-1 loop takes the medium-range trig rule inline;
+  // with a broadcast q0 out of line (trig_advance_f1: same values either way)
   if constexpr (kFrame1<SP> && !DAMPED) {
-    if (a.rec && a.S == 1 && a.q0_stride == 0) {  // collision continuation records (ikg_collision.hip)
-      hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, false, true>), grid, dim3(64), lds_pad_bytes(), s,
-                         dmodel, prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out,
-                         a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n);
+    const bool med = a.S > 1 || a.q0_stride != 0 || force_med;
+    if (a.rec) {  // collision continuation records (ikg_collision.hip)
+      if (med)
+        hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, true, true>), grid, dim3(64), lds_pad_bytes(), s,
+                           dmodel, prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw,
+                           (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n);
+      else
+        hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, false, true>), grid, dim3(64), lds_pad_bytes(), s,
+                           dmodel, prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw,
+                           (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n);
       if (a.rec_used) *a.rec_used = true;
       return;
     }
-    if (a.S > 1 || a.q0_stride != 0 || force_med) {
+    if (med) {
       hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, true>), grid, dim3(64), lds_pad_bytes(), s, dmodel,
                          prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out,
                          a.converged, a.iters, (T*)a.err_out);
@@ -344,6 +351,9 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   BatchArgs b{a.targets, a.seeds, a.S == 1 ? 0 : a.nq, a.T * a.S, a.ws_q, a.ws_conv, a.ws_iters, a.ws_err, 32, a.S};
   b.ws_owner = a.ws_owner;
   b.jit = a.jit;
+  b.rec = a.rec;
+  b.rec_n = a.rec_n;
+  b.rec_used = a.rec_used;
   // AUTO keeps the pair layout here: seeds spread the update counts, and a
   // wave lasts as long as its slowest problem -- 64 per packed wave against 32
   // per pair wave measured 4.17 ms against 3.66 ms (256 seeds x 512 targets,

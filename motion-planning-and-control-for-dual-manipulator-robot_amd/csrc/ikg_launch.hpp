@@ -174,6 +174,10 @@ struct MultiArgs {
   int variant = 0;  // ikg_variant of the per-seed solves
   const JitKernels* jit = nullptr;
   WsOwner* ws_owner = nullptr;
+  // collision continuation records for the S x T per-seed problems (BatchArgs::rec)
+  void* rec = nullptr;
+  int32_t* rec_n = nullptr;
+  bool* rec_used = nullptr;
 };
 
 // Debug knob IKG_POISON=1 (read per call): every stream-ordered workspace is

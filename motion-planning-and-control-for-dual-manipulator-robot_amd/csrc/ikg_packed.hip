@@ -115,7 +115,7 @@ static bool capped_ok() {
   if (!v) {
     int blocks = 0;
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, false>), 64, packed_lds_pad());
+        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, true>), 64, packed_lds_pad());
     v = (e == hipSuccess && blocks == 4 * WPS) ? 1 : 2;
     cache[dev].store(v, std::memory_order_relaxed);
   }
@@ -132,15 +132,15 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
                        (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out, a.converged, a.iters,
                        (float*)a.err_out);
   };
-  // per-problem seeds: the medium-range trig series (ikg_device.hpp trig_advance_f1)
-  static const bool force_med = getenv("IKG_FORCE_MED") && atoi(getenv("IKG_FORCE_MED")) != 0;  // measurement knob
-  const bool med = a.S > 1 || a.q0_stride != 0 || force_med;
+  // the medium-range trig rule inline for every launch: same values as the
+  // out-of-line form, and 2% faster at C3 under this kernel's max-ILP schedule
+  // (1.281 against 1.309 ms, profiles/r04/trig/)
   if (need == 1 && capped_ok<1>())
-    med ? go(ikg_packed_batch_kernel<SpecNextage, 1, true>) : go(ikg_packed_batch_kernel<SpecNextage, 1, false>);
+    go(ikg_packed_batch_kernel<SpecNextage, 1, true>);
   else if (need == 2 && capped_ok<2>())
-    med ? go(ikg_packed_batch_kernel<SpecNextage, 2, true>) : go(ikg_packed_batch_kernel<SpecNextage, 2, false>);
+    go(ikg_packed_batch_kernel<SpecNextage, 2, true>);
   else
-    med ? go(ikg_packed_batch_kernel<SpecNextage, 0, true>) : go(ikg_packed_batch_kernel<SpecNextage, 0, false>);
+    go(ikg_packed_batch_kernel<SpecNextage, 0, true>);
   return hipGetLastError();
 }
 

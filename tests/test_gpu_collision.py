@@ -133,20 +133,41 @@ def test_multistart_with_collision_matches_single_solves(csolver, solve_cases, m
     tg = c["targets"][:16]
     seeds = np.stack([np.zeros(15)] + [c["q0"][-k] for k in range(1, 4)])
     ms = csolver.solve_multistart(tg, seeds, check_collision=True)
-    per = [csolver.solve(tg, s, check_collision=True) for s in seeds]
+    # a row per problem: the multi-start's trig rule (medium-range series), and
+    # both record in the batch kernel (round 4): bit for bit
+    per = [csolver.solve(tg, np.tile(s, (len(tg), 1)), check_collision=True) for s in seeds]
     for t in range(len(tg)):
         b = ms.best_seed[t]
         assert ms.converged[t] == per[b].converged[t]
         assert ms.converged[t] == any(p.converged[t] for p in per)
         assert ms.iters[t] == per[b].iters[t]
-        # a broadcast seed's records come from the batch kernel (trig state
-        # carried on), per-problem seeds' from the trajectory kernel (trig
-        # resynced at each window): the same iterates to rounding
-        assert np.abs(ms.q[t] - per[b].q[t]).max() <= 1e-9
-    monkeypatch.setenv("IKG_TRAJ_REC", "0")
-    per0 = [csolver.solve(tg, s, check_collision=True) for s in seeds]
+        assert np.array_equal(ms.q[t], per[b].q[t]) and np.array_equal(ms.err[t], per[b].err[t])
+    # a broadcast seed: the exact-sincos rule for medium steps, so rounding only
+    bc = [csolver.solve(tg, s, check_collision=True) for s in seeds]
     for t in range(len(tg)):
-        assert np.array_equal(ms.q[t], per0[ms.best_seed[t]].q[t])  # same schedule: bit for bit
+        b = ms.best_seed[t]
+        assert ms.converged[t] == bc[b].converged[t] and ms.iters[t] == bc[b].iters[t]
+        assert np.abs(ms.q[t] - bc[b].q[t]).max() <= 1e-9
+    monkeypatch.setenv("IKG_TRAJ_REC", "0")
+    per0 = [csolver.solve(tg, np.tile(s, (len(tg), 1)), check_collision=True) for s in seeds]
+    ms0 = csolver.solve_multistart(tg, seeds, check_collision=True)
+    for t in range(len(tg)):
+        assert np.array_equal(ms0.q[t], per0[ms0.best_seed[t]].q[t])  # trajectory schedule: bit for bit
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_collision_answer_does_not_depend_on_q0_layout(csolver, solve_cases, dtype):
+    """with the collision term, a broadcast q0 and a row per problem
+    both record in the batch kernel (round 4), so from q0 = 0 the same problem
+    gets the same bits either way; per-row runs of one seed equal the
+    multi-start's (test above)."""
+    c = solve_cases
+    seed = c["q0"][0]
+    assert not seed.any()
+    a = csolver.solve(c["targets"], seed, dtype=dtype, check_collision=True)
+    b = csolver.solve(c["targets"], np.tile(seed, (len(c["targets"]), 1)), dtype=dtype, check_collision=True)
+    for x, y in zip((a.q, a.converged, a.iters, a.err), (b.q, b.converged, b.iters, b.err)):
+        assert np.array_equal(x, y)
 
 
 def test_check_collision_without_scene_fails_loudly(solver):

@@ -87,11 +87,11 @@ def test_emulated_damped_variant_matches_damped_oracle(emu, kat):
 
 @pytest.mark.parametrize("dtype", [0, 1])
 def test_medium_trig_series_matches_exact_fallback(emu, dtype):
-    """Random seeds take large first steps: the medium-range series
+    """Random seeds take large first steps.  The medium-range series
     (Trig::step_med, per-problem seeds) and the exact-sincos fallback (broadcast
-    q0) must give the same iterates.  Compared over the first 150 updates, before
-    the non-converging solves' chaotic drift amplifies rounding: q within 1e-10
-    (fp64) / 1e-3 (fp32)."""
+    q0) must give the same iterates to rounding.  Compared over the first 150
+    updates, before the non-converging solves' chaotic drift amplifies rounding:
+    q within 1e-10 (fp64) / 1e-3 (fp32)."""
     from ikgrasp.workload import random_seeds, uniform_targets
     tg = uniform_targets(6, seed=31)
     for seed in random_seeds(load_nextage(), 3, seed=32):
