@@ -2198,6 +2198,10 @@ __device__ inline void pinv_step_lq(const T (&A)[6][8], int, T* dq, T& s) {
 #ifndef IKG_COLD_CALL
 #define IKG_COLD_CALL 1
 #endif
+// the fp32 / packed kernels' guard branch out of line too (round 4 A/B)
+#ifndef IKG_COLD_F32
+#define IKG_COLD_F32 0
+#endif
 template <typename T>
 struct ColdIO {  // the branch's inputs and outputs, copied only when it is taken
   ArmStateF1<T> st;
@@ -2222,7 +2226,7 @@ __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restri
   pinv_step_tail<T, X>(u, v, alpha, beta, m->sing_beta, dq, s, need);
   if (__builtin_expect(IKG_SING_GUARD && need, 0)) {
 #if IKG_COLD_CALL
-    if constexpr (is_f64<T> && COLD) {  // fp64 only: the fp32 kernels measured 2-10% slower with the call
+    if constexpr ((is_f64<T> || IKG_COLD_F32) && COLD) {  // fp32: IKG_COLD_F32 (measured, see IKG_COLD_F32)
       ColdIO<T> io;
       io.st = st;
 #pragma unroll

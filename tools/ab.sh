@@ -18,6 +18,7 @@ for c in ${CONFIGS:-c2_f64 c2_f64_forced c3_f32 rand_f64}; do
     c4s_f64) run $c 6 131072 f64 ABL_EPS=1e-3 ;;
     c4s_f32) run $c 6 131072 f32 ABL_EPS=1e-3 ;;
     rand_f64) run $c 6 131072 f64 ABL_EPS=1e-3 ABL_RANDQ0=1 ;;
+    rand_f32) run $c 6 131072 f32 ABL_EPS=1e-3 ABL_RANDQ0=1 ;;
     c2col_f64) run $c 10 4096 f64 ABL_EPS=1e-3 ABL_COLLISION=1 ;;
     *) echo "unknown config $c"; exit 2 ;;
   esac
