@@ -1789,6 +1789,15 @@ IKG_HD inline bool beyond(float x, float b) {
   return __builtin_bit_cast(uint32_t, x) > __builtin_bit_cast(uint32_t, b);
 }
 IKG_HD inline v2i beyond(v2f x, float b) { return v2i{beyond(x.x, b) ? -1 : 0, beyond(x.y, b) ? -1 : 0}; }
+// The guard over this lane's and the partner arm's |v|^2.  A packed lane
+// holds both arms, so the partner's is its own other half: one unsigned max and
+// one compare instead of two masked 2-vectors (round 4: 10 fewer VALU per update).
+IKG_HD inline bool guard_test(double x, double xo, double b) { return beyond(x, b) || beyond(xo, b); }
+IKG_HD inline bool guard_test(float x, float xo, float b) { return beyond(x, b) || beyond(xo, b); }
+IKG_HD inline bool guard_test(v2f x, v2f, float b) {
+  const uint32_t hx = __builtin_bit_cast(uint32_t, x.x), hy = __builtin_bit_cast(uint32_t, x.y);
+  return (hx > hy ? hx : hy) > __builtin_bit_cast(uint32_t, b);
+}
 
 // ---------------------------------------------------------------- singular arm blocks
 // pinv(J) e for J = [c | blockdiag(J_L, J_R)] without inverting the arm
@@ -2175,7 +2184,7 @@ __device__ inline void pinv_step_tail(const T* u, const T* v, T alpha, T beta, t
   const T bo = xc(beta);
   s = chest_step(alpha + xc(alpha), beta + bo);
   arm_dq(u, v, s, dq);
-  need = any_of(mor(beyond(beta, bound), beyond(bo, bound)));
+  need = guard_test(beta, bo, bound);
 }
 
 template <typename T, class X = PairX>
@@ -2198,10 +2207,6 @@ __device__ inline void pinv_step_lq(const T (&A)[6][8], int, T* dq, T& s) {
 #ifndef IKG_COLD_CALL
 #define IKG_COLD_CALL 1
 #endif
-// the fp32 / packed kernels' guard branch out of line too (round 4 A/B)
-#ifndef IKG_COLD_F32
-#define IKG_COLD_F32 0
-#endif
 template <typename T>
 struct ColdIO {  // the branch's inputs and outputs, copied only when it is taken
   ArmStateF1<T> st;
@@ -2215,8 +2220,10 @@ __device__ __attribute__((noinline)) void pinv_step_f1_cold(const KModel<typenam
   pinv_step_lq<T, X>(A, arm, io->dq, io->s);
 }
 
-// COLD: the out-of-line branch (fp64 only); the records-in-batch loop (REC)
-// measured 3% slower with it at C2 with the collision term, so it inlines
+// COLD: the out-of-line branch, for fp64 and the packed fp32 layout; the pair
+// fp32 kernel keeps it inline (the call measured +0.4% at C2 fp32, DESIGN
+// §3a.5), and so does the records-in-batch loop (REC: 3% slower with it at C2
+// with the collision term)
 template <typename T, class SP, class X = PairX, bool COLD = true>
 __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restrict__ m, int arm, const ArmStateF1<T>& st,
                                     const T* sn, const T* cs, T* dq, T& s) {
@@ -2226,7 +2233,7 @@ __device__ inline void pinv_step_f1(const KModel<typename LaneT<T>::E>* __restri
   pinv_step_tail<T, X>(u, v, alpha, beta, m->sing_beta, dq, s, need);
   if (__builtin_expect(IKG_SING_GUARD && need, 0)) {
 #if IKG_COLD_CALL
-    if constexpr ((is_f64<T> || IKG_COLD_F32) && COLD) {  // fp32: IKG_COLD_F32 (measured, see IKG_COLD_F32)
+    if constexpr ((is_f64<T> || is_packed<T>) && COLD) {
       ColdIO<T> io;
       io.st = st;
 #pragma unroll

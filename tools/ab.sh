@@ -19,6 +19,7 @@ for c in ${CONFIGS:-c2_f64 c2_f64_forced c3_f32 rand_f64}; do
     c4s_f32) run $c 6 131072 f32 ABL_EPS=1e-3 ;;
     rand_f64) run $c 6 131072 f64 ABL_EPS=1e-3 ABL_RANDQ0=1 ;;
     rand_f32) run $c 6 131072 f32 ABL_EPS=1e-3 ABL_RANDQ0=1 ;;
+    big_f32) run $c 3 1048576 f32 ABL_EPS=1e-3 ABL_RANDQ0=1 ;;     # C5-sized launch (3+ waves per SIMD)
     c2col_f64) run $c 10 4096 f64 ABL_EPS=1e-3 ABL_COLLISION=1 ;;
     *) echo "unknown config $c"; exit 2 ;;
   esac

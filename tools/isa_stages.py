@@ -125,7 +125,11 @@ def main(path, kname, show_blocks):
         if bm and bm.group(2) in pos and cur in pos and pos[bm.group(2)] <= pos[cur]:
             back.append((pos[cur] - pos[bm.group(2)], bm.group(2), cur))
     back.sort(reverse=True)
-    _, head, tail = back[0]
+    # the update loop: the widest backward branch whose span holds arm_update
+    # (the singular branch's Jacobi sweeps can be wider and hold none)
+    def has_update(h, t):
+        return any(stage_of(c) == "arm_update" for b in order[pos[h]:pos[t] + 1] for _, c in blocks.get(b, []))
+    _, head, tail = next((x for x in back if has_update(x[1], x[2])), back[0])
     loop = order[pos[head]:pos[tail] + 1]
     tot = collections.Counter()
     fn = collections.Counter()
