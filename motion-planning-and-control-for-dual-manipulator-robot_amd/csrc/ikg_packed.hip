@@ -29,7 +29,10 @@ namespace ikg {
 // tools/placement_probe.py).  The launcher checks the resulting occupancy.
 // (amdgpu_waves_per_eu: the guarded step's cold LQ branch spills instead of
 // raising the allocation of the loop: 157 VGPRs, 3 waves per SIMD)
-template <class SP, int WPS, bool MED>
+// REC: the collision continuation's records (ikg_collision.hip §3b), written
+// from the first passing iterate on, both arms' blocks by the problem's lane;
+// the outputs at that iterate come from its record 0 (solve_pair).
+template <class SP, int WPS, bool MED, bool REC = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPS == 0 ? 3 : WPS)))
 void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               KParams<float> prm, const float* __restrict__ targets,
@@ -37,7 +40,8 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               int64_t B, int64_t S, float* __restrict__ q_out,
                                                               uint8_t* __restrict__ conv_out,
                                                               int32_t* __restrict__ iters_out,
-                                                              float* __restrict__ err_out) {
+                                                              float* __restrict__ err_out, float* __restrict__ rec = nullptr,
+                                                              int32_t* __restrict__ rec_n = nullptr) {
   if constexpr (WPS == 1) asm volatile("" ::: "a255");
   // v171: at least 172 VGPRs, so 2 waves fit and 3 do not; an AGPR claim
   // instead makes the allocator split the 2-wave budget 128 VGPR / 128 AGPR
@@ -56,7 +60,16 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
   int it;
   bool conv;
   v2f nrm, other;
-  solve_pair<v2f, false, SP, MED>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
+  if constexpr (REC) {
+    const int rl = rec_len(m->n_passive);
+    const RecOut<float> ro{rec + p * (int64_t)(prm.max_iters + 1) * rl, rec_n + p, qrow, q_out + p * m->nq,
+                           conv_out + p, iters_out + p, err_out + p * 2, rl};
+    rec_n[p] = 0;
+    solve_pair<v2f, false, SP, MED, true>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro);
+    if (conv) return;
+  } else {
+    solve_pair<v2f, false, SP, MED>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
+  }
   float* qo = q_out + p * m->nq;
   qo[m->root_q] = qc.x;
   for (int i = 0; i < m->n_passive; ++i) {  // moved only by the first update's clamp (tools.py:21-22)
@@ -105,7 +118,7 @@ static unsigned simd_count() {
 
 // The cap instantiation really fits WPS waves per SIMD (4 WPS single-wave
 // workgroups per CU) on this device; otherwise the uncapped kernel runs.
-template <int WPS>
+template <int WPS, bool REC = false>
 static bool capped_ok() {
   constexpr int kDevs = 64;
   static std::atomic<int> cache[kDevs];  // 0 unknown, 1 ok, 2 not
@@ -115,7 +128,7 @@ static bool capped_ok() {
   if (!v) {
     int blocks = 0;
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, true>), 64, packed_lds_pad());
+        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, true, REC>), 64, packed_lds_pad());
     v = (e == hipSuccess && blocks == 4 * WPS) ? 1 : 2;
     cache[dev].store(v, std::memory_order_relaxed);
   }
@@ -130,8 +143,21 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(64), packed_lds_pad(), s, dmodel, prm, (const float*)a.targets,
                        (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out, a.converged, a.iters,
-                       (float*)a.err_out);
+                       (float*)a.err_out, (float*)a.rec, a.rec_n);
   };
+#ifndef IKG_PACKED_REC
+#define IKG_PACKED_REC 1
+#endif
+  if (IKG_PACKED_REC && a.rec) {  // collision continuation records (0: A/B knob, the trajectory kernel instead)
+    if (need == 1 && capped_ok<1, true>())
+      go(ikg_packed_batch_kernel<SpecNextage, 1, true, true>);
+    else if (need == 2 && capped_ok<2, true>())
+      go(ikg_packed_batch_kernel<SpecNextage, 2, true, true>);
+    else
+      go(ikg_packed_batch_kernel<SpecNextage, 0, true, true>);
+    if (a.rec_used) *a.rec_used = true;
+    return hipGetLastError();
+  }
   // the medium-range trig rule inline for every launch: same values as the
   // out-of-line form, and 2% faster at C3 under this kernel's max-ILP schedule
   // (1.281 against 1.309 ms, profiles/r04/trig/)

@@ -105,8 +105,7 @@ template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
 __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
                                   const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
                                   T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out,
-                                  const RecOut<T>* ro = nullptr) {
-  static_assert(!REC || !is_packed<T>, "records: pair layout only");
+                                  const RecOut<typename LaneT<T>::E>* ro = nullptr) {
   int k0 = -1;  // REC: the first iterate whose errors pass
   static_assert(!(DAMPED && is_packed<T>), "the packed layout implements lambda = 0 only");
   constexpr bool F1 = kFrame1<SP> && !DAMPED;  // frame-1 path, its own trig slots
@@ -176,12 +175,28 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
         conv = true;
       }
       if (k0 >= 0) {
-        T blk[8];
-        blk[0] = arm ? (pass ? T(1) : T(0)) : qc;
+        if constexpr (is_packed<T>) {  // both arms' blocks from the one lane
+          float b0[8], b1[8];
+          b0[0] = qc.x;
+          b1[0] = pass ? 1.f : 0.f;
 #pragma unroll
-        for (int k = 0; k < kArmDof; ++k) blk[1 + k] = qa[k];
-        blk[7] = x;
-        store_block8(ro->rec + (int64_t)(it - k0) * ro->rl + (arm ? kRecPass : kRecRoot), blk);
+          for (int k = 0; k < kArmDof; ++k) {
+            b0[1 + k] = qa[k].x;
+            b1[1 + k] = qa[k].y;
+          }
+          b0[7] = x.x;
+          b1[7] = x.y;
+          float* dst = ro->rec + (int64_t)(it - k0) * ro->rl;
+          store_block8(dst + kRecRoot, b0);
+          store_block8(dst + kRecPass, b1);
+        } else {
+          T blk[8];
+          blk[0] = arm ? (pass ? T(1) : T(0)) : qc;
+#pragma unroll
+          for (int k = 0; k < kArmDof; ++k) blk[1 + k] = qa[k];
+          blk[7] = x;
+          store_block8(ro->rec + (int64_t)(it - k0) * ro->rl + (arm ? kRecPass : kRecRoot), blk);
+        }
       }
       if (ended) break;
     } else {
@@ -213,6 +228,21 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
       // the outputs at the first passing iterate, from its record (this lane's
       // own block of record 0): writing them inside the loop put a divergent
       // branch into every update (records-in-batch kernel 4% slower)
+      if constexpr (is_packed<T>) {
+        float b[2][8], qa0[kArmDof];
+        load_block8(ro->rec + kRecRoot, b[0]);
+        load_block8(ro->rec + kRecPass, b[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+#pragma unroll
+          for (int k = 0; k < kArmDof; ++k) qa0[k] = b[h][1 + k];
+          store_q(m, h, ro->qrow, k0, b[0][0], qa0, ro->qo);
+          ro->err[h] = sqrtf(b[h][7]);
+        }
+        *ro->conv = 1;
+        *ro->iters = k0;
+        *ro->nrec = (it - k0 + 1) | kTrajEnded;
+      } else {
       T blk[8];
       load_block8(ro->rec + (arm ? kRecPass : kRecRoot), blk);
       T qa0[kArmDof];
@@ -224,6 +254,7 @@ __device__ inline void solve_pair(const KModel<typename LaneT<T>::E>* __restrict
         *ro->conv = 1;
         *ro->iters = k0;
         *ro->nrec = (it - k0 + 1) | kTrajEnded;
+      }
       }
     }
   }

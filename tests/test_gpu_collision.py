@@ -275,6 +275,35 @@ def test_records_in_batch_kernel_equal_trajectory_kernel(csolver, dtype, monkeyp
 
 
 @pytest.mark.parametrize("poison", ["0", "1"])
+def test_packed_kernel_records_equal_trajectory_kernel(csolver, monkeypatch, poison):
+    """The packed fp32 kernel writes the records itself (both arms' blocks from
+    one lane) when they fit the budget: C2's 4,096 targets from q = 0 in the
+    packed layout, its records against the trajectory kernel's recomputed ones
+    (same flags and update counts; q to fp32 rounding: the trajectory kernel
+    resyncs its trig per window), deterministic, and nothing read before it
+    is written (IKG_POISON=1)."""
+    from ikgrasp import _lib
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(4096, seed=0)
+    monkeypatch.setenv("IKG_POISON", poison)
+    monkeypatch.setenv("IKG_TRAJ_REC", "1")
+    kw = dict(dtype="f32", check_collision=True, variant=_lib.IKG_VARIANT_PACKED)
+    a = csolver.solve(tg, np.zeros(15), **kw)
+    a2 = csolver.solve(tg, np.zeros(15), **kw)
+    assert np.array_equal(a.q, a2.q) and np.array_equal(a.iters, a2.iters)
+    monkeypatch.setenv("IKG_TRAJ_REC", "0")
+    b = csolver.solve(tg, np.zeros(15), **kw)
+    same = (a.converged == b.converged) & (a.iters == b.iters)
+    print(f"packed records vs trajectory kernel: {int((~same).sum())} of 4096 differ in flag or count")
+    assert same.mean() >= 0.999
+    assert np.abs(a.q[same] - b.q[same]).max() <= 1e-3
+    # converged without the collision term but not with it: ran on to max_iters (:70)
+    free = csolver.solve(tg, np.zeros(15), dtype="f32", variant=_lib.IKG_VARIANT_PACKED)
+    cont = free.converged & ~a.converged
+    assert cont.sum() >= 100 and (a.iters[cont] == 1000).all()
+
+
+@pytest.mark.parametrize("poison", ["0", "1"])
 def test_trajectory_window_ending_at_max_iters(csolver, solve_cases, oracle_cases, monkeypatch, poison):
     """A record window that stops exactly at update max_iters without having
     recorded that iterate (k0 + m * Wn == max_iters) must hand it to the next

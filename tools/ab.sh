@@ -21,6 +21,14 @@ for c in ${CONFIGS:-c2_f64 c2_f64_forced c3_f32 rand_f64}; do
     rand_f32) run $c 6 131072 f32 ABL_EPS=1e-3 ABL_RANDQ0=1 ;;
     big_f32) run $c 3 1048576 f32 ABL_EPS=1e-3 ABL_RANDQ0=1 ;;     # C5-sized launch (3+ waves per SIMD)
     c2col_f64) run $c 10 4096 f64 ABL_EPS=1e-3 ABL_COLLISION=1 ;;
+    c3col_f32) run $c 6 65536 f32 ABL_EPS=1e-3 ABL_COLLISION=1 ;;
+    c3colrec_f32) run $c 6 65536 f32 ABL_EPS=1e-3 ABL_COLLISION=1 IKG_REC_BUDGET_MB=8192 IKG_REC_PREFER_PAIR=1 ;;
+    c4scol_f64) run $c 4 131072 f64 ABL_EPS=1e-3 ABL_COLLISION=1 ;;
+    c3colbig_f32) run $c 6 65536 f32 ABL_EPS=1e-3 ABL_COLLISION=1 IKG_REC_BUDGET_MB=8192 ;;  # records if the layout writes them
+    c2col_f64_nopool) run $c 10 4096 f64 ABL_EPS=1e-3 ABL_COLLISION=1 IKG_WS_POOL=0 ;;
+    c3col_f32_nopool) run $c 6 65536 f32 ABL_EPS=1e-3 ABL_COLLISION=1 IKG_WS_POOL=0 ;;
+    c3colbig_f32_nopool) run $c 6 65536 f32 ABL_EPS=1e-3 ABL_COLLISION=1 IKG_REC_BUDGET_MB=8192 IKG_WS_POOL=0 ;;
+    c2colpk_f32) run $c 10 4096 f32 ABL_EPS=1e-3 ABL_COLLISION=1 ABL_VARIANT=2 ;;           # packed layout at C2
     *) echo "unknown config $c"; exit 2 ;;
   esac
 done

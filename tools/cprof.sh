@@ -1,7 +1,9 @@
 #!/bin/bash
-# Build the phase-timing diagnostic library (gitignored, travels with gpurun).
+# Build the phase-timing diagnostic library (gitignored, travels with gpurun):
+# the shipped per-file flags (Makefile) plus -DIKG_CPROF.
 set -e
 cd "$(dirname "$0")/../motion-planning-and-control-for-dual-manipulator-robot_amd/csrc"
 mkdir -p ../ikgrasp/_native/abl
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -fno-slp-vectorize -Xarch_device -ffinite-math-only -Xarch_device -fno-signed-zeros -Xarch_device -Wno-nan-infinity-disabled -DIKG_CPROF -I../../include -I. \
-  -shared -o ../ikgrasp/_native/abl/libikgrasp_cprof.so ikg_kernels.hip ikg_packed.hip ikg_quad.hip ikg_collision.hip ikg_control.hip ikg_jit.hip ikg_capi.hip -ldl
+make -s build/ikg_jit_src.inc
+make -s -j8 BUILD=build_cprof EXTRA="-DIKG_CPROF" OUT=../ikgrasp/_native/abl/libikgrasp_cprof.so ../ikgrasp/_native/abl/libikgrasp_cprof.so
+rm -rf build_cprof

@@ -13,3 +13,5 @@ for i in $(seq 1 12); do
   fi
   exit $rc
 done
+echo "[gpurun_retry: no box after 12 tries]" >> "$log"
+exit 3

@@ -8,7 +8,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "motion-planning-and-control-for-dual-manipulator-robot_amd")
-os.environ["IKGRASP_LIB"] = os.path.join(PKG, "ikgrasp/_native/abl/libikgrasp_cprof.so")
+os.environ.setdefault("IKGRASP_LIB", os.path.join(PKG, "ikgrasp/_native/abl/libikgrasp_cprof.so"))
 sys.path.insert(0, PKG)
 
 import numpy as np  # noqa: E402
