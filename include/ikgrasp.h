@@ -31,9 +31,14 @@
  *     throws or exits across this boundary.
  *   - Calls are re-entrant per (model, stream).
  *   - Results are deterministic.  A problem's fp64 answer is the same bit for
- *     bit in any batch size, batch position and collision schedule, with
- *     one exception: a broadcast q0 (q0_stride = 0) and per-problem q0 rows
- *     (and multi-start seeds) advance the joint sin/cos by different rules for
+ *     bit in any batch size and batch position, with two exceptions.  With
+ *     the collision term, a problem that converges into collision runs on in
+ *     the batch kernel itself (records) when the batch's records fit the
+ *     record budget, else in the trajectory kernel, which resyncs the joint
+ *     sin/cos per window: the two agree to rounding (q <= 1e-9), and which
+ *     one runs depends on the batch size.  And a broadcast q0
+ *     (q0_stride = 0) and per-problem q0 rows (and multi-start seeds)
+ *     advance the joint sin/cos by different rules for
  *     steps of 0.025..0.25 rad (exact sincos / a longer series), so when such
  *     steps occur -- random seeds, not the reference's q0 = 0 on its sampler's
  *     targets -- the two agree to rounding (<= 1e-10 over 150 updates), not
@@ -52,6 +57,13 @@
  *   - All instantiations of one captured graph share that scratch: do not
  *     launch two of them concurrently (on different streams).
  *   - Destroy graphs before the model: they also reference its device tables.
+ *
+ * Scratch memory
+ *   - Uncaptured solves take their scratch from a library-owned stream-ordered
+ *     pool per device that keeps freed memory for the next solve (the
+ *     collision records are the large item, up to 1 GiB per solve).
+ *     ikg_model_destroy returns the pool's unused memory to the driver.
+ *     IKG_WS_POOL=0 in the environment selects the device's default pool.
  */
 #ifndef IKGRASP_H
 #define IKGRASP_H

@@ -227,15 +227,18 @@ ikg::KParams<T> kparams(const ikg_params* p) {
 // selects the trajectory kernel, which recomputes the updates past the first
 // passing iterate).  Its round-2 graph-replay mismatch was the graph memory
 // node the records came from (ws_alloc, ikg_launch.hpp).  Up
-// to kRecBudget bytes of records per solve.
+// to rec_budget() bytes of records per solve.
 static bool rec_in_batch() {
   const char* e = getenv("IKG_TRAJ_REC");
   return !(e && atoi(e) == 0);
 }
-constexpr size_t kRecBudget = size_t(1) << 30;
-static size_t rec_budget() {  // IKG_REC_BUDGET_MB: measurement knob
-  const char* e = getenv("IKG_REC_BUDGET_MB");
-  return e ? (size_t)atoll(e) << 20 : kRecBudget;
+// Budget 1 GiB (C2 fp64: 656 MB).  Larger budgets were measured: C3 fp32's
+// 5.2 GB of packed-kernel records scan in about the time the trajectory
+// windows take (2.21-2.39 against 2.33-2.34 ms), so the memory
+// is not spent.  IKG_REC_BUDGET_MB overrides (measurement knob).
+static size_t rec_budget() {
+  if (const char* e = getenv("IKG_REC_BUDGET_MB")) return (size_t)atoll(e) << 20;
+  return size_t(1) << 30;
 }
 
 
@@ -632,6 +635,7 @@ void ikg_model_destroy(ikg_model* m) {
   // its buffer: graphs must be destroyed before the model, whose tables they
   // also reference -- include/ikgrasp.h "Graphs")
   ikg::ws_drain(&m->ws);
+  ikg::ws_pool_trim();
   if (prev >= 0) (void)hipSetDevice(prev);
   delete m;
 }

@@ -83,9 +83,61 @@ inline void ws_drain(WsOwner* owner) {
   if (prev >= 0) (void)hipSetDevice(prev);
 }
 
+// The library's stream-ordered scratch pool, one per device, which keeps what
+// a solve frees (release threshold: all of it) for the next solve instead of
+// returning it to the driver at every synchronisation, as the device's default
+// pool does (threshold 0): a collision solve's record buffer (656 MB at C2,
+// 5 GB at C3 fp32 with a raised budget) was otherwise mapped afresh on every
+// call.  ikg_model_destroy trims it.  IKG_WS_POOL=0: the default pool (A/B).
+struct WsPools {
+  static constexpr int kDevs = 64;
+  std::mutex mu;
+  hipMemPool_t pool[kDevs] = {};
+};
+inline WsPools& ws_pools() {
+  static WsPools p;
+  return p;
+}
+inline hipMemPool_t ws_pool() {
+  static const bool on = !(getenv("IKG_WS_POOL") && atoi(getenv("IKG_WS_POOL")) == 0);
+  if (!on) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= WsPools::kDevs) return nullptr;
+  WsPools& P = ws_pools();
+  std::lock_guard<std::mutex> lock(P.mu);
+  if (!P.pool[dev]) {
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    uint64_t keep = UINT64_MAX;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    P.pool[dev] = pool;
+  }
+  return P.pool[dev];
+}
+
+// give every pool's cached memory back to the driver (ikg_model_destroy; the
+// memory of solves still in flight on other models stays allocated)
+inline void ws_pool_trim() {
+  WsPools& P = ws_pools();
+  std::lock_guard<std::mutex> lock(P.mu);
+  for (int d = 0; d < WsPools::kDevs; ++d)
+    if (P.pool[d]) (void)hipMemPoolTrimTo(P.pool[d], 0);
+}
+
 inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s) {
   *p = nullptr;
-  if (!owner || !stream_capturing(s)) return hipMallocAsync(p, bytes, s);
+  if (!owner || !stream_capturing(s)) {
+    if (hipMemPool_t pool = ws_pool()) return hipMallocFromPoolAsync(p, bytes, pool, s);
+    return hipMallocAsync(p, bytes, s);
+  }
   hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
   hipGraph_t graph = nullptr;
   hipError_t e = hipStreamGetCaptureInfo_v2(s, &cst, nullptr, &graph, nullptr, nullptr);
