@@ -29,6 +29,7 @@ for c in ${CONFIGS:-c2_f64 c2_f64_forced c3_f32 rand_f64}; do
     c3col_f32_nopool) run $c 6 65536 f32 ABL_EPS=1e-3 ABL_COLLISION=1 IKG_WS_POOL=0 ;;
     c3colbig_f32_nopool) run $c 6 65536 f32 ABL_EPS=1e-3 ABL_COLLISION=1 IKG_REC_BUDGET_MB=8192 IKG_WS_POOL=0 ;;
     c5col_f32) run $c 3 512 f32 ABL_EPS=1e-3 ABL_COLLISION=1 ABL_MS=256 ;;                  # C5 share: 256 seeds x 512 targets
+    c2col_f32) run $c 10 4096 f32 ABL_EPS=1e-3 ABL_COLLISION=1 ;;
     c2colpk_f32) run $c 10 4096 f32 ABL_EPS=1e-3 ABL_COLLISION=1 ABL_VARIANT=2 ;;           # packed layout at C2
     *) echo "unknown config $c"; exit 2 ;;
   esac
