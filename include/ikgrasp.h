@@ -59,10 +59,11 @@
  *   - Destroy graphs before the model: they also reference its device tables.
  *
  * Scratch memory
- *   - Uncaptured solves take their scratch from a library-owned stream-ordered
- *     pool per device that keeps freed memory for the next solve (the
- *     collision records are the large item, up to 1 GiB per solve).
- *     ikg_model_destroy returns the pool's unused memory to the driver.
+ *   - Uncaptured solves take their scratch from a stream-ordered pool the
+ *     model owns (one per device it solves on) that keeps freed memory for
+ *     the next solve (the collision records are the large item, up to 1 GiB
+ *     per solve).  ikg_model_destroy synchronises each such device and
+ *     destroys the pools, which returns the memory to the driver.
  *     IKG_WS_POOL=0 in the environment selects the device's default pool.
  */
 #ifndef IKGRASP_H

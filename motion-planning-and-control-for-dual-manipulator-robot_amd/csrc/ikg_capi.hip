@@ -635,7 +635,7 @@ void ikg_model_destroy(ikg_model* m) {
   // its buffer: graphs must be destroyed before the model, whose tables they
   // also reference -- include/ikgrasp.h "Graphs")
   ikg::ws_drain(&m->ws);
-  ikg::ws_pool_trim();
+  ikg::ws_pool_release(&m->ws);
   if (prev >= 0) (void)hipSetDevice(prev);
   delete m;
 }

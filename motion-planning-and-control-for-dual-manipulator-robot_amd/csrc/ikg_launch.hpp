@@ -34,9 +34,11 @@ struct JitKernels;  // ikg_jit.hpp
 // shares its scratch, so two of them must not run at the same time
 // (include/ikgrasp.h, "Graphs").
 struct WsState {
+  static constexpr int kDevs = 64;
   std::mutex mu;
   std::vector<std::pair<int, void*>> pending;  // (device, pointer) whose graphs are gone
   int64_t live = 0;                            // buffers held by graphs
+  hipMemPool_t pool[kDevs] = {};               // the model's scratch pools (ws_pool), per device
 };
 
 struct WsOwner {
@@ -83,29 +85,21 @@ inline void ws_drain(WsOwner* owner) {
   if (prev >= 0) (void)hipSetDevice(prev);
 }
 
-// The library's stream-ordered scratch pool, one per device, which keeps what
-// a solve frees (release threshold: all of it) for the next solve instead of
-// returning it to the driver at every synchronisation, as the device's default
-// pool does (threshold 0): a collision solve's record buffer (656 MB at C2,
-// 5 GB at C3 fp32 with a raised budget) was otherwise mapped afresh on every
-// call.  ikg_model_destroy trims it.  IKG_WS_POOL=0: the default pool (A/B).
-struct WsPools {
-  static constexpr int kDevs = 64;
-  std::mutex mu;
-  hipMemPool_t pool[kDevs] = {};
-};
-inline WsPools& ws_pools() {
-  static WsPools p;
-  return p;
-}
-inline hipMemPool_t ws_pool() {
+// The model's stream-ordered scratch pool, one per device it solves on, which
+// keeps what a solve frees (release threshold: all of it) for the next solve
+// instead of returning it to the driver at every synchronisation, as the
+// device's default pool does (threshold 0): a collision solve's record buffer
+// (656 MB at C2) was otherwise mapped afresh on every call.  The pools are the
+// model's: ikg_model_destroy destroys them (ws_pool_release), which gives the
+// memory back.  IKG_WS_POOL=0: the device's default pool (A/B).
+inline hipMemPool_t ws_pool(WsOwner* owner) {
   static const bool on = !(getenv("IKG_WS_POOL") && atoi(getenv("IKG_WS_POOL")) == 0);
-  if (!on) return nullptr;
+  if (!on || !owner) return nullptr;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= WsPools::kDevs) return nullptr;
-  WsPools& P = ws_pools();
-  std::lock_guard<std::mutex> lock(P.mu);
-  if (!P.pool[dev]) {
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= WsState::kDevs) return nullptr;
+  WsState& st = *owner->st;
+  std::lock_guard<std::mutex> lock(st.mu);
+  if (!st.pool[dev]) {
     hipMemPoolProps props = {};
     props.allocType = hipMemAllocationTypePinned;
     props.handleTypes = hipMemHandleTypeNone;
@@ -118,24 +112,30 @@ inline hipMemPool_t ws_pool() {
     }
     uint64_t keep = UINT64_MAX;
     (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    P.pool[dev] = pool;
+    st.pool[dev] = pool;
   }
-  return P.pool[dev];
+  return st.pool[dev];
 }
 
-// give every pool's cached memory back to the driver (ikg_model_destroy; the
-// memory of solves still in flight on other models stays allocated)
-inline void ws_pool_trim() {
-  WsPools& P = ws_pools();
-  std::lock_guard<std::mutex> lock(P.mu);
-  for (int d = 0; d < WsPools::kDevs; ++d)
-    if (P.pool[d]) (void)hipMemPoolTrimTo(P.pool[d], 0);
+// Destroy the model's pools (ikg_model_destroy): each device is synchronised
+// first, so the stream-ordered frees of its last solves have run.
+inline void ws_pool_release(WsOwner* owner) {
+  if (!owner) return;
+  WsState& st = *owner->st;
+  std::lock_guard<std::mutex> lock(st.mu);
+  for (int d = 0; d < WsState::kDevs; ++d)
+    if (st.pool[d]) {
+      (void)hipSetDevice(d);
+      (void)hipDeviceSynchronize();
+      (void)hipMemPoolDestroy(st.pool[d]);
+      st.pool[d] = nullptr;
+    }
 }
 
 inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s) {
   *p = nullptr;
   if (!owner || !stream_capturing(s)) {
-    if (hipMemPool_t pool = ws_pool()) return hipMallocFromPoolAsync(p, bytes, pool, s);
+    if (hipMemPool_t pool = ws_pool(owner)) return hipMallocFromPoolAsync(p, bytes, pool, s);
     return hipMallocAsync(p, bytes, s);
   }
   hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
