@@ -27,8 +27,9 @@ namespace ikg {
 // some kernels (after the collision continuation, 19-46 of 1,024 SIMDs held two
 // waves of the next 1,024-wave launch and the kernel took 2.2 ms instead of 1.4;
 // tools/placement_probe.py).  The launcher checks the resulting occupancy.
-// (amdgpu_waves_per_eu: the guarded step's cold LQ branch spills instead of
-// raising the allocation of the loop: 157 VGPRs, 3 waves per SIMD)
+// (amdgpu_waves_per_eu bounds the allocation at the occupancy the cap allows;
+// the guarded step's LQ branch is an out-of-line call, and its spills and
+// stack frame are touched only when it is taken -- DESIGN.md §3a.5)
 // REC: the collision continuation's records (ikg_collision.hip §3b), written
 // from the first passing iterate on, both arms' blocks by the problem's lane;
 // the outputs at that iterate come from its record 0 (solve_pair).
