@@ -546,9 +546,19 @@ def main():
         rl, rl_hbm = roofline(args.dtype, "packed" if packed else "pair", bool(S), kern_ms, sum_iters,
                               -(-B * max(S, 1) // ppw), cus * 4, abytes, traffic, tsrc)
         if args.collision:
-            rl["kernel"] = kname + " (records every iterate past the first passing one) + ikg_prescreen_kernel + " \
-                                   "ikg_traj_scan_kernel"
-            rl["kernel_ms_covers"] = "the whole solve: batch kernel, pre-screen, compaction, record scan"
+            # the batch kernel records the run-on iterates when they fit the record budget
+            # (ikg_capi.hip rec_budget: 1 GiB, 20 values per iterate), else the trajectory kernel
+            # recomputes them in windows
+            budget = int(os.environ.get("IKG_REC_BUDGET_MB", "1024")) << 20
+            rec_bytes = (8 if args.dtype == "f64" else 4) * 20 * 1001 * B * max(S, 1)
+            if rec_bytes <= budget:
+                rl["kernel"] = kname + " (records every iterate past the first passing one) + " \
+                                       "ikg_prescreen_kernel + ikg_traj_scan_kernel"
+                rl["kernel_ms_covers"] = "the whole solve: batch kernel, pre-screen, compaction, record scan"
+            else:
+                rl["kernel"] = kname + " + ikg_prescreen_kernel + ikg_traj_kernel (the run-on iterates " \
+                                       "recomputed and scanned in windows: records exceed the budget)"
+                rl["kernel_ms_covers"] = "the whole solve: batch kernel, pre-screen, compaction, trajectory windows"
         else:
             rl["kernel"] = kname
         parallelism = f"shard{world}"
