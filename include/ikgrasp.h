@@ -36,14 +36,16 @@
  *     the batch kernel itself (records) when the batch's records fit the
  *     record budget, else in the trajectory kernel, which resyncs the joint
  *     sin/cos per window: the two agree to rounding (q <= 1e-9), and which
- *     one runs depends on the batch size.  And a broadcast q0
+ *     one runs depends on the batch size.  And in fp64 a broadcast q0
  *     (q0_stride = 0) and per-problem q0 rows (and multi-start seeds)
- *     advance the joint sin/cos by different rules for
- *     steps of 0.025..0.25 rad (exact sincos / a longer series), so when such
- *     steps occur -- random seeds, not the reference's q0 = 0 on its sampler's
- *     targets -- the two agree to rounding (<= 1e-10 over 150 updates), not
- *     bit for bit.  A multi-start's seed equals a per-row solve of that seed
- *     bit for bit.  fp32 results also depend on the kernel layout (PAIR /
+ *     advance the joint sin/cos by different rules for steps of
+ *     0.025..0.25 rad (exact sincos / a longer series), so when such steps
+ *     occur -- random seeds, not the reference's q0 = 0 on its sampler's
+ *     targets -- the two agree to rounding (q <= 1e-10, end effectors
+ *     <= 1e-12 over 150 updates), not bit for bit.  fp32 takes the longer
+ *     series for every q0 layout: its answer does not depend on how q0 is
+ *     passed.  A multi-start's seed equals a per-row solve of that seed bit
+ *     for bit.  fp32 results also depend on the kernel layout (PAIR /
  *     PACKED), which AUTO picks by batch size.
  *
  * Graphs
@@ -51,20 +53,27 @@
  *     hipGraph (no host synchronisation, no blocking allocation).  Scratch a
  *     captured solve needs (records, multi-start and continuation workspaces)
  *     is allocated at capture time and owned by the captured graph (a graph
- *     user object): it is released when the graph and all its executable
- *     instantiations are destroyed, and freed by the model's next uncaptured
- *     solve or by ikg_model_destroy.
+ *     user object).  When the graph and all its executable instantiations
+ *     are destroyed the buffer goes on the model's pending list: a later
+ *     capture on the model reuses it if it is large enough (so recapturing
+ *     every cycle holds a bounded number of buffers), and the model's next
+ *     uncaptured solve, ikg_model_trim or ikg_model_destroy frees it.
  *   - All instantiations of one captured graph share that scratch: do not
  *     launch two of them concurrently (on different streams).
  *   - Destroy graphs before the model: they also reference its device tables.
  *
  * Scratch memory
  *   - Uncaptured solves take their scratch from a stream-ordered pool the
- *     model owns (one per device it solves on) that keeps freed memory for
- *     the next solve (the collision records are the large item, up to 1 GiB
- *     per solve).  ikg_model_destroy synchronises each such device and
- *     destroys the pools, which returns the memory to the driver.
- *     IKG_WS_POOL=0 in the environment selects the device's default pool.
+ *     model owns (one per device it solves on).  The pool keeps up to
+ *     1.25 GiB of freed memory mapped for the next solve (the collision
+ *     records are the large item, up to 1 GiB per solve; environment
+ *     IKG_WS_KEEP_MB overrides the amount) and returns the rest to the
+ *     driver at the next synchronisation.  ikg_model_trim synchronises each
+ *     such device and returns everything the pools hold unused;
+ *     ikg_model_destroy synchronises and destroys the pools.  Either leaves
+ *     the device's free memory where it was before the model's first solve
+ *     (tests/test_gpu_memory.py).  IKG_WS_POOL=0 in the environment selects
+ *     the device's default pool.
  */
 #ifndef IKGRASP_H
 #define IKGRASP_H
@@ -158,6 +167,12 @@ typedef struct ikg_model ikg_model;
 /* Build a device-ready model (tables are uploaded to every device lazily). */
 int ikg_model_create(const ikg_model_desc* desc, ikg_model** out);
 void ikg_model_destroy(ikg_model* model);
+
+/* Return the scratch memory the model's pools keep for later solves (and the
+ * buffers of destroyed captured graphs) to the driver; the model stays usable.
+ * Synchronises every device the model has solved on.  No reference
+ * counterpart (the reference allocates nothing on a device). */
+int ikg_model_trim(ikg_model* model);
 
 /* Attach (or replace) the collision scene of a model. */
 int ikg_model_set_collision(ikg_model* model, const ikg_collision_desc* desc);

@@ -555,8 +555,9 @@ int ikg_log6_batch(int device, int dtype, const void* M, int64_t B, void* out, v
 const char* ikg_last_error(void) { return g_err; }
 
 // Diagnostic (not in include/ikgrasp.h): scratch buffers held by captured
-// graphs (live) and those whose graphs are gone, freed on the model's next
-// uncaptured solve (pending).  tests/test_gpu_graph.py.
+// graphs (live) and those whose graphs are gone (pending: reused by the next
+// capture, freed by the model's next uncaptured solve or ikg_model_trim).
+// tests/test_gpu_graph.py.
 int ikg_debug_ws_count(const ikg_model* model, int64_t* live, int64_t* pending) {
   if (!model || !live || !pending) return fail(IKG_EINVAL, "bad arguments");
   std::lock_guard<std::mutex> lock(model->ws.st->mu);
@@ -638,6 +639,17 @@ void ikg_model_destroy(ikg_model* m) {
   ikg::ws_pool_release(&m->ws);
   if (prev >= 0) (void)hipSetDevice(prev);
   delete m;
+}
+
+int ikg_model_trim(ikg_model* m) {
+  g_err[0] = 0;
+  if (!m) return fail(IKG_EINVAL, "model is NULL");
+  int prev = -1;
+  (void)hipGetDevice(&prev);
+  ikg::ws_drain(&m->ws);  // buffers of destroyed graphs
+  const hipError_t e = ikg::ws_pool_trim(&m->ws);
+  if (prev >= 0) (void)hipSetDevice(prev);
+  return e == hipSuccess ? IKG_OK : hip_fail(e, "ikg_model_trim");
 }
 
 int ikg_solve_batch(const ikg_model* model, int device, int dtype, const void* targets, const void* q0,

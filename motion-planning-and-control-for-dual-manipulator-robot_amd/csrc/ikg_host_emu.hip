@@ -199,9 +199,10 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
     const T* qr = (const T*)q0 + stride * i;
     T* tr = trace ? (T*)trace + (int64_t)2 * trace_len * i : nullptr;
     if (spec == 1)
-      // the kernels' medium-range trig series for per-problem seeds (ikg_kernels.hip)
+      // the kernels' medium-range trig series for per-problem seeds, and for
+      // every fp32 solve (ikg_kernels.hip launch_pair_batch_t)
       emu_one<T, ikg::SpecNextage>(m, prm, p->lambda > 0, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
-                                   (T*)err + 2 * i, tr, trace_len, col, stride != 0);
+                                   (T*)err + 2 * i, tr, trace_len, col, stride != 0 || sizeof(T) == 4);
     else if (spec == 2 && !(p->lambda > 0))
       emu_one<T, ikg::SpecGenericWrist>(m, prm, false, tg, qr, (T*)q_out + d->nq * i, conv + i, iters + i,
                                         (T*)err + 2 * i, tr, trace_len, col);

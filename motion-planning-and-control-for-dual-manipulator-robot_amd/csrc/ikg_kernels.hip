@@ -216,10 +216,13 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
   // IKG_FORCE_MED=1: measurement knob, the inline medium-range rule for every launch
   static const bool force_med = getenv("IKG_FORCE_MED") && atoi(getenv("IKG_FORCE_MED")) != 0;
   // per-problem seeds (multi-start, or a q0 row per target): large first steps
-  // are common, so the frame-1 loop takes the medium-range trig rule inline;
-  // with a broadcast q0 out of line (trig_advance_f1: same values either way)
+  // are common, so the frame-1 loop takes the medium-range trig rule inline.
+  // fp64 with a broadcast q0 keeps the short-series rule (exact sincos beyond
+  // its range: 4% faster at C2, the same values to rounding); fp32 takes the
+  // medium-range rule for every q0 layout, as the packed kernel does, so an
+  // fp32 answer does not depend on how q0 was passed
   if constexpr (kFrame1<SP> && !DAMPED) {
-    const bool med = a.S > 1 || a.q0_stride != 0 || force_med;
+    const bool med = a.S > 1 || a.q0_stride != 0 || force_med || std::is_same<T, float>::value;
     if (a.rec) {  // collision continuation records (ikg_collision.hip)
       if (med)
         hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, true, true>), grid, dim3(64), lds_pad_bytes(), s,
@@ -311,7 +314,7 @@ hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, con
   if (a.variant == IKG_VARIANT_PACKED) return hipErrorInvalidValue;  // checked by the C-ABI first
   const bool damped = prm.lambda > T(0);
   if (a.jit) {  // the pair loop compiled against this model's constant tables (ikg_jit.hip)
-    const bool med = a.S > 1 || a.q0_stride != 0;
+    const bool med = a.S > 1 || a.q0_stride != 0 || std::is_same<T, float>::value;
     hipFunction_t f = damped ? a.jit->damped : (med && a.jit->pair_med ? a.jit->pair_med : a.jit->pair);
     const T* targets = (const T*)a.targets;
     const T* q0 = (const T*)a.q0;

@@ -28,17 +28,26 @@ struct JitKernels;  // ikg_jit.hpp
 // the call) and hands it to the capturing graph as a user object
 // (hipGraphRetainUserObject): the buffer lives exactly as long as the graph
 // and its executable instantiations.  The user object's destructor may not
-// call HIP, so it only queues the buffer on the model's pending list; the
-// next uncaptured call into the library on that model (or
-// ikg_model_destroy) frees it.  Every instantiation of one captured graph
-// shares its scratch, so two of them must not run at the same time
-// (include/ikgrasp.h, "Graphs").
+// call HIP, so it only queues the buffer on the model's pending list.  A
+// later capture takes a pending buffer that is large enough instead of
+// allocating (no HIP call), so a workload that recaptures every cycle and
+// never solves uncaptured holds a bounded number of buffers; the rest are
+// freed by the model's next uncaptured call, ikg_model_trim or
+// ikg_model_destroy.  Every instantiation of one captured graph shares its
+// scratch, so two of them must not run at the same time (include/ikgrasp.h,
+// "Graphs").
+struct WsBuf {
+  int dev;
+  void* p;
+  size_t bytes;
+};
+
 struct WsState {
   static constexpr int kDevs = 64;
   std::mutex mu;
-  std::vector<std::pair<int, void*>> pending;  // (device, pointer) whose graphs are gone
-  int64_t live = 0;                            // buffers held by graphs
-  hipMemPool_t pool[kDevs] = {};               // the model's scratch pools (ws_pool), per device
+  std::vector<WsBuf> pending;     // buffers whose graphs are gone
+  int64_t live = 0;               // buffers held by graphs
+  hipMemPool_t pool[kDevs] = {};  // the model's scratch pools (ws_pool), per device
 };
 
 struct WsOwner {
@@ -47,15 +56,14 @@ struct WsOwner {
 
 struct GraphScratch {  // one captured buffer, owned by its graph's user object
   std::shared_ptr<WsState> st;
-  int dev;
-  void* p;
+  WsBuf b;
 };
 
 inline void graph_scratch_release(void* arg) {  // user-object destructor: no HIP calls here
   GraphScratch* g = static_cast<GraphScratch*>(arg);
   {
     std::lock_guard<std::mutex> lock(g->st->mu);
-    g->st->pending.emplace_back(g->dev, g->p);
+    g->st->pending.push_back(g->b);
     --g->st->live;
   }
   delete g;
@@ -70,7 +78,7 @@ inline bool stream_capturing(hipStream_t s) {
 // calling thread's stream is capturing: hipFree is not a capturable call).
 inline void ws_drain(WsOwner* owner) {
   if (!owner) return;
-  std::vector<std::pair<int, void*>> v;
+  std::vector<WsBuf> v;
   {
     std::lock_guard<std::mutex> lock(owner->st->mu);
     v.swap(owner->st->pending);
@@ -79,19 +87,50 @@ inline void ws_drain(WsOwner* owner) {
   int prev = -1;
   (void)hipGetDevice(&prev);
   for (auto& b : v) {
-    (void)hipSetDevice(b.first);
-    (void)hipFree(b.second);
+    (void)hipSetDevice(b.dev);
+    (void)hipFree(b.p);
   }
   if (prev >= 0) (void)hipSetDevice(prev);
 }
 
+// The smallest pending buffer on `dev` of at least `bytes`, taken off the
+// list (a capture reuses it: no HIP call), or null.
+inline void* ws_take_pending(WsState& st, int dev, size_t bytes, size_t* got) {
+  std::lock_guard<std::mutex> lock(st.mu);
+  int best = -1;
+  for (int i = 0; i < (int)st.pending.size(); ++i) {
+    const WsBuf& b = st.pending[i];
+    if (b.dev == dev && b.bytes >= bytes && (best < 0 || b.bytes < st.pending[best].bytes)) best = i;
+  }
+  if (best < 0) return nullptr;
+  const WsBuf b = st.pending[best];
+  st.pending.erase(st.pending.begin() + best);
+  *got = b.bytes;
+  return b.p;
+}
+
+// How much freed scratch a model's pool keeps mapped across synchronisations
+// (its release threshold): 1.25 GiB by default -- the collision records
+// budget (1 GiB, ikg_capi.hip rec_budget) plus the continuation's workspaces,
+// so a solve that repeats finds its scratch in the pool -- and anything above
+// that goes back to the driver at the next synchronisation.
+// IKG_WS_KEEP_MB overrides (0 = keep nothing, as the device's default pool).
+inline uint64_t ws_keep_bytes() {
+  static const uint64_t v = [] {
+    const char* e = getenv("IKG_WS_KEEP_MB");
+    return e ? (uint64_t)strtoull(e, nullptr, 10) << 20 : (uint64_t)1280 << 20;
+  }();
+  return v;
+}
+
 // The model's stream-ordered scratch pool, one per device it solves on, which
-// keeps what a solve frees (release threshold: all of it) for the next solve
-// instead of returning it to the driver at every synchronisation, as the
-// device's default pool does (threshold 0): a collision solve's record buffer
-// (656 MB at C2) was otherwise mapped afresh on every call.  The pools are the
-// model's: ikg_model_destroy destroys them (ws_pool_release), which gives the
-// memory back.  IKG_WS_POOL=0: the device's default pool (A/B).
+// keeps what a solve frees (up to ws_keep_bytes) for the next solve instead of
+// returning it to the driver at every synchronisation, as the device's default
+// pool does (threshold 0): a collision solve's record buffer (656 MB at C2)
+// was otherwise mapped afresh on every call (1-1.5% of a collision solve).
+// The pools are the model's: ikg_model_trim returns their unused memory,
+// ikg_model_destroy destroys them (ws_pool_release).  IKG_WS_POOL=0: the
+// device's default pool (A/B).
 inline hipMemPool_t ws_pool(WsOwner* owner) {
   static const bool on = !(getenv("IKG_WS_POOL") && atoi(getenv("IKG_WS_POOL")) == 0);
   if (!on || !owner) return nullptr;
@@ -110,26 +149,52 @@ inline hipMemPool_t ws_pool(WsOwner* owner) {
       (void)hipGetLastError();
       return nullptr;
     }
-    uint64_t keep = UINT64_MAX;
+    uint64_t keep = ws_keep_bytes();
     (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     st.pool[dev] = pool;
   }
   return st.pool[dev];
 }
 
-// Destroy the model's pools (ikg_model_destroy): each device is synchronised
-// first, so the stream-ordered frees of its last solves have run.
-inline void ws_pool_release(WsOwner* owner) {
-  if (!owner) return;
+// Every device the model has a pool on, with the pool handles copied out
+// under the lock (`take`: and cleared, for ws_pool_release).  The callers
+// synchronise and call into HIP outside the lock: graph_scratch_release takes
+// the same mutex and may run on a runtime thread while a device synchronises.
+inline std::vector<std::pair<int, hipMemPool_t>> ws_pools(WsOwner* owner, bool take) {
+  std::vector<std::pair<int, hipMemPool_t>> v;
+  if (!owner) return v;
   WsState& st = *owner->st;
   std::lock_guard<std::mutex> lock(st.mu);
   for (int d = 0; d < WsState::kDevs; ++d)
     if (st.pool[d]) {
-      (void)hipSetDevice(d);
-      (void)hipDeviceSynchronize();
-      (void)hipMemPoolDestroy(st.pool[d]);
-      st.pool[d] = nullptr;
+      v.emplace_back(d, st.pool[d]);
+      if (take) st.pool[d] = nullptr;
     }
+  return v;
+}
+
+// Destroy the model's pools (ikg_model_destroy): each device is synchronised
+// first, so the stream-ordered frees of its last solves have run.
+inline void ws_pool_release(WsOwner* owner) {
+  for (auto& dp : ws_pools(owner, true)) {
+    (void)hipSetDevice(dp.first);
+    (void)hipDeviceSynchronize();
+    (void)hipMemPoolDestroy(dp.second);
+  }
+}
+
+// Return the pools' unused memory to the driver (ikg_model_trim): each device
+// is synchronised, then its pool trimmed to nothing kept; the pool stays
+// usable.
+inline hipError_t ws_pool_trim(WsOwner* owner) {
+  hipError_t rc = hipSuccess;
+  for (auto& dp : ws_pools(owner, false)) {
+    (void)hipSetDevice(dp.first);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemPoolTrimTo(dp.second, 0);
+    if (e != hipSuccess && rc == hipSuccess) rc = e;
+  }
+  return rc;
 }
 
 inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s) {
@@ -142,17 +207,22 @@ inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s
   hipGraph_t graph = nullptr;
   hipError_t e = hipStreamGetCaptureInfo_v2(s, &cst, nullptr, &graph, nullptr, nullptr);
   if (e != hipSuccess || !graph) return e != hipSuccess ? e : hipErrorStreamCaptureInvalidated;
-  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
-  (void)hipThreadExchangeStreamCaptureMode(&mode);
-  e = hipMalloc(p, bytes ? bytes : 1);
-  (void)hipThreadExchangeStreamCaptureMode(&mode);
-  if (e != hipSuccess) {
-    *p = nullptr;
-    return e;
-  }
   int dev = 0;
   (void)hipGetDevice(&dev);
-  GraphScratch* g = new GraphScratch{owner->st, dev, *p};
+  const size_t want = bytes ? bytes : 1;
+  size_t got = want;
+  *p = ws_take_pending(*owner->st, dev, want, &got);  // a destroyed graph's buffer
+  if (!*p) {
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    e = hipMalloc(p, want);
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    if (e != hipSuccess) {
+      *p = nullptr;
+      return e;
+    }
+  }
+  GraphScratch* g = new GraphScratch{owner->st, WsBuf{dev, *p, got}};
   hipUserObject_t uo = nullptr;
   e = hipUserObjectCreate(&uo, g, graph_scratch_release, 1, hipUserObjectNoDestructorSync);
   if (e == hipSuccess) {
@@ -165,10 +235,10 @@ inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s
     return e;
   }
   delete g;
-  mode = hipStreamCaptureModeRelaxed;
-  (void)hipThreadExchangeStreamCaptureMode(&mode);
-  (void)hipFree(*p);
-  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  {  // back on the pending list: freed by the next uncaptured call
+    std::lock_guard<std::mutex> lock(owner->st->mu);
+    owner->st->pending.push_back(WsBuf{dev, *p, got});
+  }
   *p = nullptr;
   return e;
 }

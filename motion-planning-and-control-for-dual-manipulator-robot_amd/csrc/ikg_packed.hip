@@ -159,9 +159,11 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
     if (a.rec_used) *a.rec_used = true;
     return hipGetLastError();
   }
-  // the medium-range trig rule inline for every launch: same values as the
-  // out-of-line form, and 2% faster at C3 under this kernel's max-ILP schedule
-  // (1.281 against 1.309 ms, profiles/r04/trig/)
+  // the medium-range trig rule inline for every launch (and every q0 layout,
+  // as the fp32 pair kernel): it agrees with the short-series-or-exact rule
+  // to rounding, not bit for bit, on steps of 0.025..0.25 rad, and is 2%
+  // faster at C3 under this kernel's max-ILP schedule (1.281 against 1.309 ms,
+  // profiles/r04/trig/)
   if (need == 1 && capped_ok<1>())
     go(ikg_packed_batch_kernel<SpecNextage, 1, true>);
   else if (need == 2 && capped_ok<2>())

@@ -84,7 +84,7 @@ EXPORTS = [
     "ikg_model_create", "ikg_model_destroy", "ikg_params_default", "ikg_solve_batch",
     "ikg_solve_multistart", "ikg_fk_batch", "ikg_log6_batch", "ikg_last_error", "ikg_version",
     "ikg_model_set_collision", "ikg_collision_batch", "ikg_distance_batch", "ikg_target_env_batch",
-    "ikg_frame_kinematics_batch", "ikg_model_specialize", "ikg_model_is_specialized",
+    "ikg_frame_kinematics_batch", "ikg_model_specialize", "ikg_model_is_specialized", "ikg_model_trim",
 ]
 
 _lib = None
@@ -123,6 +123,8 @@ def load() -> C.CDLL:
     lib.ikg_model_create.restype = i32
     lib.ikg_model_destroy.argtypes = [vp]
     lib.ikg_model_destroy.restype = None
+    lib.ikg_model_trim.argtypes = [vp]
+    lib.ikg_model_trim.restype = i32
     lib.ikg_params_default.argtypes = [C.POINTER(Params)]
     lib.ikg_params_default.restype = None
     lib.ikg_solve_batch.argtypes = [vp, i32, i32, vp, vp, i64, i64, C.POINTER(Params), vp, vp, vp, vp, vp,

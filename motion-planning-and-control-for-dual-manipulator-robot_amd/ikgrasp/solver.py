@@ -123,6 +123,11 @@ class IKSolver:
         code, _ = _dtype(dtype)
         return bool(self.lib.ikg_model_is_specialized(self._h, self.device if device is None else device, code))
 
+    def trim(self):
+        """Give the scratch memory this model's pools keep for later solves
+        back to the driver (ikg_model_trim); the solver stays usable."""
+        _lib.check(self.lib.ikg_model_trim(self._h))
+
     def close(self):
         if getattr(self, "_h", None) is not None and self._h.value:
             self.lib.ikg_model_destroy(self._h)

@@ -155,6 +155,34 @@ def test_multistart_with_collision_matches_single_solves(csolver, solve_cases, m
         assert np.array_equal(ms0.q[t], per0[ms0.best_seed[t]].q[t])  # trajectory schedule: bit for bit
 
 
+def test_multistart_packed_with_collision_matches_per_row_packed(csolver, solve_cases, monkeypatch):
+    """a multi-start with variant PACKED and the collision term
+    (the packed kernel records S > 1 seeds in the batch kernel) equals
+    per-row packed solves of each seed bit for bit, and a broadcast seed too
+    (fp32 takes the medium-range trig rule for every q0 layout); against the
+    trajectory kernel (IKG_TRAJ_REC=0, which resyncs its trig per window) the
+    flags and counts agree and q to fp32 rounding."""
+    from ikgrasp import _lib
+    c = solve_cases
+    tg = c["targets"][:64]
+    seeds = np.stack([np.zeros(15)] + [c["q0"][-k] for k in range(1, 4)])
+    kw = dict(dtype="f32", check_collision=True, variant=_lib.IKG_VARIANT_PACKED)
+    monkeypatch.setenv("IKG_TRAJ_REC", "1")
+    ms = csolver.solve_multistart(tg, seeds, **kw)
+    per = [csolver.solve(tg, np.tile(s, (len(tg), 1)), **kw) for s in seeds]
+    bc = [csolver.solve(tg, s, **kw) for s in seeds]
+    for t in range(len(tg)):
+        b = ms.best_seed[t]
+        for p in (per[b], bc[b]):
+            assert ms.converged[t] == p.converged[t] and ms.iters[t] == p.iters[t]
+            assert np.array_equal(ms.q[t], p.q[t]) and np.array_equal(ms.err[t], p.err[t])
+    monkeypatch.setenv("IKG_TRAJ_REC", "0")
+    ms0 = csolver.solve_multistart(tg, seeds, **kw)
+    same = (ms0.converged == ms.converged) & (ms0.iters == ms.iters) & (ms0.best_seed == ms.best_seed)
+    assert same.mean() >= 0.95, int((~same).sum())
+    assert np.abs(ms0.q[same] - ms.q[same]).max() <= 1e-3
+
+
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_collision_answer_does_not_depend_on_q0_layout(csolver, solve_cases, dtype):
     """with the collision term, a broadcast q0 and a row per problem

@@ -209,20 +209,34 @@ def test_broadcast_q0_equals_explicit(solver):
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_q0_layout_from_random_seeds(solver, dtype):
-    """A broadcast q0 and a row per problem run different trig rules for steps
-    of 0.025..0.25 rad (exact sincos / medium-range series, ikg_device.hpp
-    trig_advance_f1): the same iterates to rounding.  Compared over the first
-    150 updates, before non-converging solves' chaotic drift: identical flags
-    and counts, q within 1e-10 (fp64) / 1e-2 (fp32).  From q0 = 0 (no such
-    steps) the two are bit-equal (test_broadcast_q0_equals_explicit)."""
+    """A broadcast q0 and a row per problem give one answer per problem.
+    fp32 advances the joint sin/cos by the medium-range rule for every q0
+    layout: identical bits.  fp64 keeps two rules for steps of 0.025..0.25 rad
+    (exact sincos for a broadcast q0, the medium-range series for rows;
+    ikg_device.hpp trig_advance_f1): the same iterates to rounding, compared
+    over the first 150 updates, before non-converging solves' chaotic drift --
+    identical flags and counts, q within 1e-10 and the end effectors within
+    north_star's 1e-4 SE(3) tolerance (measured ~1e-12).  From q0 = 0 (no such
+    steps) the two are bit-equal in both dtypes
+    (test_broadcast_q0_equals_explicit)."""
     from ikgrasp.workload import random_seeds, uniform_targets
     tg = uniform_targets(256, seed=6)
+    ee_max = 0.0
     for seed in random_seeds(solver.model, 4, seed=7):
         a = solver.solve(tg, seed, dtype=dtype, max_iters=150)
         b = solver.solve(tg, np.tile(seed, (256, 1)), dtype=dtype, max_iters=150)
         assert np.array_equal(a.converged, b.converged) and np.array_equal(a.iters, b.iters)
-        # fp32: ~6e-8 relative per medium step, amplified by poorly scaled seeds (measured 1.6e-3)
-        assert np.abs(a.q - b.q).max() <= (1e-10 if dtype == "f64" else 1e-2)
+        if dtype == "f32":
+            assert np.array_equal(a.q, b.q)
+            continue
+        assert np.abs(a.q - b.q).max() <= 1e-10
+        ha, hb = solver.fk(a.q), solver.fk(b.q)
+        for h in range(2):
+            e = helpers.se3_err(ha[:, h, :9].reshape(-1, 3, 3), ha[:, h, 9:], hb[:, h, :9].reshape(-1, 3, 3),
+                                hb[:, h, 9:])
+            ee_max = max(ee_max, float(e.max()))
+    print(f"q0 layouts, {dtype}: end-effector SE(3) distance max {ee_max:.2e}")
+    assert ee_max <= 1e-4  # north_star: 1e-4 end-effector SE(3) error
 
 
 def test_empty_batch(solver):

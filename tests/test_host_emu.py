@@ -33,6 +33,7 @@ def emu():
         B = len(tg)
         # per-row q0 (stride 15) runs the kernels' medium-range trig series, a
         # broadcast q0 (stride 0) the short series with the exact fallback
+        # (fp64; fp32 takes the medium-range series either way)
         q0 = np.ascontiguousarray(q0 if broadcast else np.broadcast_to(q0, (B, 15)), dtype=npt)
         stride = 0 if broadcast else 15
         p = _lib.default_params(**kw)
@@ -87,18 +88,22 @@ def test_emulated_damped_variant_matches_damped_oracle(emu, kat):
 
 @pytest.mark.parametrize("dtype", [0, 1])
 def test_medium_trig_series_matches_exact_fallback(emu, dtype):
-    """Random seeds take large first steps.  The medium-range series
+    """Random seeds take large first steps.  fp64: the medium-range series
     (Trig::step_med, per-problem seeds) and the exact-sincos fallback (broadcast
-    q0) must give the same iterates to rounding.  Compared over the first 150
+    q0) must give the same iterates to rounding -- compared over the first 150
     updates, before the non-converging solves' chaotic drift amplifies rounding:
-    q within 1e-10 (fp64) / 1e-3 (fp32)."""
+    q within 1e-10.  fp32 runs the medium-range series for both layouts, as the
+    kernels do: identical bits."""
     from ikgrasp.workload import random_seeds, uniform_targets
     tg = uniform_targets(6, seed=31)
     for seed in random_seeds(load_nextage(), 3, seed=32):
         a = emu(tg, seed, dtype=dtype, max_iters=150)
         b = emu(tg, seed, dtype=dtype, broadcast=True, max_iters=150)
         assert np.array_equal(a[1], b[1]) and np.array_equal(a[2], b[2])
-        assert np.abs(a[0] - b[0]).max() <= (1e-10 if dtype == 0 else 1e-3)
+        if dtype == 0:
+            assert np.abs(a[0] - b[0]).max() <= 1e-10
+        else:
+            assert np.array_equal(a[0], b[0])
 
 
 def _emu_math(fn, x, y=None):
