@@ -195,10 +195,11 @@ def flops_profile(kernel, dtype, med):
     return None
 
 
-def hbm_profile(dtype, B, S=0, collision=False):
+def hbm_profile(dtype, B, S=0, collision=False, variant=""):
     """Counter HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE) for this
     configuration, from profiles/pmc_*.json, or None."""
-    tag = f"pmc_{dtype}_b{B}" + (f"_s{S}" if S else "") + ("_col" if collision else "") + ".json"
+    tag = (f"pmc_{dtype}_b{B}" + (f"_s{S}" if S else "") + ("_col" if collision else "") +
+           (f"_{variant}" if variant else "") + ".json")
     p = os.path.join(ROOT, "profiles", tag)
     if os.path.exists(p):
         with open(p) as f:
@@ -223,7 +224,38 @@ def multistart_bytes(dtype, T, S, nq=15):
     return T * per_target + S * nq * s + T * S * per_problem
 
 
-def roofline(dtype, kernel, med, kern_ms, sum_iters, waves, simds, abytes, traffic, traffic_src):
+SHADER_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md); the latency model's cycles -> ms
+
+
+def latency_block(kernel, dtype, med, kern_ms, max_iters, waves, simds):
+    """The bound that actually binds a launch with at most one wave per SIMD:
+    one wave's in-order issue of an update's instruction stream, times the
+    updates of the longest-running wave.  Per-update cycles come from the
+    committed ISA model (tools/isa_critpath.py: the hot loop's instructions
+    issued in order, a VALU op at most every 4 cycles, each waiting for its
+    operands at the measured gfx950 latencies), the updates and the kernel
+    time from this run."""
+    p = os.path.join(ROOT, "profiles", f"latency_{kernel}_{dtype}{'_med' if med else ''}.json")
+    if not os.path.exists(p) or not max_iters or waves > simds:
+        return None
+    with open(p) as f:
+        m = json.load(f)
+    pred = max_iters * m["in_order_cycles"] / (SHADER_GHZ * 1e6)
+    return {
+        "bound": "per-wave in-order issue of one update's dependent instruction stream (waves <= SIMDs)",
+        "updates_longest_wave": max_iters,
+        "instructions_per_update": m["instructions_per_update"], "valu_per_update": m["valu_per_update"],
+        "issue_bound_cycles_per_update": m["issue_bound_cycles"],
+        "critical_path_cycles_per_update": m["critical_path_cycles"],
+        "model_cycles_per_update": m["in_order_cycles"], "stall_cycles_per_update": m["stall_cycles"],
+        "register_copies_per_update": m.get("register_copies_per_update"),
+        "clock_GHz": SHADER_GHZ, "predicted_ms": pred, "measured_ms": kern_ms,
+        "measured_cycles_per_update": kern_ms * SHADER_GHZ * 1e6 / max_iters,
+        "frac": pred / kern_ms, "source": os.path.relpath(p, ROOT),
+    }
+
+
+def roofline(dtype, kernel, med, kern_ms, sum_iters, waves, simds, abytes, traffic, traffic_src, max_iters=None):
     """The dominant kernel's VALU roofline (SURVEY count and executed count)
     and its HBM figures (algorithmic bytes and counter bytes), for ONE GPU:
     `sum_iters`, `waves`, `abytes` and `traffic` are that GPU's, `kern_ms` its
@@ -245,6 +277,9 @@ def roofline(dtype, kernel, med, kern_ms, sum_iters, waves, simds, abytes, traff
     if frac and frac > 1:
         out["note"] = ("frac > 1: the kernel's closed-form frame-1 loop executes fewer FP ops than the "
                        "reference formulation it is priced at (see executed)")
+    lat = latency_block(kernel, dtype, med, kern_ms, max_iters, waves, simds)
+    if lat:
+        out["latency"] = lat
     hbm = {"bound": "hbm", "algorithmic_bytes": abytes,
            "algorithmic_GBps": abytes / (kern_ms * 1e-3) / 1e9, "peak": PEAK_HBM, "unit": "GB/s",
            "traffic": traffic, "traffic_source": traffic_src}
@@ -505,6 +540,7 @@ def main():
 
     n_conv = int(conv.sum().item())
     sum_iters = int(iters.to(torch.int64).sum().item())
+    max_iters = int(iters.max().item()) if B else 0
     if S:
         # the multi-start launch returns the winner's update count only; its per-seed solves are
         # exactly ikg_solve_batch over the expanded (target, seed) problems (same kernel, same
@@ -544,7 +580,8 @@ def main():
         abytes = algorithmic_bytes(args.dtype, B) if not S else multistart_bytes(args.dtype, B, S)
         traffic, tsrc = hbm_profile(args.dtype, B, S, args.collision)
         rl, rl_hbm = roofline(args.dtype, "packed" if packed else "pair", bool(S), kern_ms, sum_iters,
-                              -(-B * max(S, 1) // ppw), cus * 4, abytes, traffic, tsrc)
+                              -(-B * max(S, 1) // ppw), cus * 4, abytes, traffic, tsrc,
+                              max_iters=None if (S or args.collision) else max_iters)
         if args.collision:
             # the batch kernel records the run-on iterates when they fit the record budget
             # (ikg_capi.hip rec_budget: 1 GiB, 20 values per iterate), else the trajectory kernel
@@ -646,8 +683,8 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
         ps = el4 / steps4
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         # rank 0's shard, priced like the headline (one GPU's updates over its kernel time)
-        rl4, _ = roofline("f64", "pair", False, km4_local, it4_local, -(-n // 32), cus * 4,
-                          algorithmic_bytes("f64", n), None, None)
+        rl4, rl4_hbm = roofline("f64", "pair", False, km4_local, it4_local, -(-n // 32), cus * 4,
+                                algorithmic_bytes("f64", n), *hbm_profile("f64", n, 0, False))
         rl4["kernel"] = "ikg_pair_batch_kernel (rank 0's shard)"
         extra["c4_strong"] = {
             "workload": f"BASELINE configs[3]: {tot} targets (uniform_targets seed 7) split over {world} rank(s), "
@@ -657,7 +694,7 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
             "value": conv4 / ps, "unit": "converged solves/s", "problems_per_s": tot / ps,
             "ms_per_step": ps * 1e3, "kernel_ms_max_rank": km4, "scaling": "strong", "n_gpus": world,
             "steps": steps4, "converged_fraction": conv4 / tot,
-            "roofline": rl4,
+            "roofline": rl4, "roofline_hbm": rl4_hbm,
             "ranks": rank_block(per4, world, "nccl" if not host else "gloo", g4,
                                 "blocking gather_rows of q, flags and update counts of the whole batch to rank 0, "
                                 "wall ms"),
@@ -714,13 +751,15 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
 
     ely, kmy_local = timed(torch, dist, world, args.steps, args.warmup, stepy, stream)
     ity_local = int(ic.to(torch.int64).sum().item())
+    ity_max = int(ic.max().item())
     ely, kmy, convy, ity = reduce_stats(torch, dist, world, host, dev,
                                         [ely, kmy_local, int(cc.sum().item()), ity_local], 2)
     if rank == 0:
         ps = ely / args.steps
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         rl, rl_hbm = roofline("f64", "pair", False, kmy_local, ity_local, -(-B // 32), cus * 4,
-                              algorithmic_bytes("f64", B), None, None)
+                              algorithmic_bytes("f64", B), *hbm_profile("f64", B, 0, False, "yaw"),
+                              max_iters=ity_max)
         rl["kernel"] = "ikg_pair_batch_kernel"
         extra["c2_yaw"] = {
             "workload": f"BASELINE configs[1], random SE(3) reading: batch {B} per GPU, fp64, cube yaw ~ "

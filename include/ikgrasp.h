@@ -65,15 +65,17 @@
  * Scratch memory
  *   - Uncaptured solves take their scratch from a stream-ordered pool the
  *     model owns (one per device it solves on).  The pool keeps up to
- *     1.25 GiB of freed memory mapped for the next solve (the collision
+ *     1.25 GiB of freed memory reserved for the next solve (the collision
  *     records are the large item, up to 1 GiB per solve; environment
- *     IKG_WS_KEEP_MB overrides the amount) and returns the rest to the
- *     driver at the next synchronisation.  ikg_model_trim synchronises each
- *     such device and returns everything the pools hold unused;
- *     ikg_model_destroy synchronises and destroys the pools.  Either leaves
- *     the device's free memory where it was before the model's first solve
- *     (tests/test_gpu_memory.py).  IKG_WS_POOL=0 in the environment selects
- *     the device's default pool.
+ *     IKG_WS_KEEP_MB overrides the amount) and releases the rest at the next
+ *     synchronisation.  ikg_model_trim synchronises each such device and
+ *     releases everything the pools hold unused; ikg_model_destroy
+ *     synchronises and destroys the pools.  Released memory goes back to the
+ *     HIP runtime, which may keep it mapped for later pools and allocations
+ *     of the process (the device's free-memory figure then does not rise);
+ *     a destroyed model leaves that figure where it was before the model
+ *     existed (tests/test_gpu_memory.py).  IKG_WS_POOL=0 in the environment
+ *     selects the device's default pool.
  */
 #ifndef IKGRASP_H
 #define IKGRASP_H

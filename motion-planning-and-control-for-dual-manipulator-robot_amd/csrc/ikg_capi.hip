@@ -242,24 +242,53 @@ static size_t rec_budget() {
 }
 
 
-// Records of the collision continuation for `n` problems (see solve_batch_t),
-// or null when they exceed the budget (the continuation then recomputes the
-// iterates past the first passing one: the trajectory kernel).
+// Records of the collision continuation for `n` problems (see solve_batch_t).
+// Fixed slots, (max_iters + 1) records per problem, when they fit the record
+// budget (C2 fp64: 656 MB); otherwise a pool of the budget's size that the
+// problems reserve from when their errors first pass (ikg_solve.hpp RecPool:
+// only the converged ones record, max_iters + 1 - k0 records each; C3 fp32
+// needs ~0.4 GB of its fixed 5.2 GB), a problem that finds it full is handed
+// to the trajectory kernel (IKG_REC_POOL=0: no pool, the trajectory kernel
+// for the whole batch, as before round 5).  Null when nothing is offered.
+static bool rec_pool_on() {
+  const char* e = getenv("IKG_REC_POOL");
+  return !(e && atoi(e) == 0);
+}
+
 template <typename T>
 void* offer_records(ikg_model* model, ikg::BatchArgs& a, const ikg_params& params, int64_t n, int nq, hipStream_t s,
                     bool* rec_used) {
   const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
-  const size_t b_rec = (sizeof(T) * rl * ((size_t)params.max_iters + 1) * (size_t)n + 255) & ~(size_t)255;
+  const size_t b_fixed = (sizeof(T) * rl * ((size_t)params.max_iters + 1) * (size_t)n + 255) & ~(size_t)255;
+  const bool pooled = b_fixed > rec_budget();
+  if (pooled && !rec_pool_on()) return nullptr;
+  const size_t b_rec = pooled ? (rec_budget() / (sizeof(T) * rl)) * sizeof(T) * rl : b_fixed;
+  const size_t b_n = (sizeof(int32_t) * (size_t)n + 255) & ~(size_t)255;
+  const size_t bytes = b_rec + b_n + (pooled ? b_n + 256 : 0);
   void* rec = nullptr;
-  if (b_rec > rec_budget() || ikg::ws_alloc(&model->ws, &rec, b_rec + sizeof(int32_t) * (size_t)n, s) != hipSuccess) {
+  if (ikg::ws_alloc(&model->ws, &rec, bytes, s) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
   a.rec = rec;
   a.rec_n = (int32_t*)((char*)rec + b_rec);
-  ikg::ws_trace("alloc rec", rec, b_rec + sizeof(int32_t) * (size_t)n, s);
+  ikg::ws_trace("alloc rec", rec, bytes, s);
   ikg::poison_float(rec, b_rec, s);
   ikg::poison_int(a.rec_n, sizeof(int32_t) * (size_t)n, s);
+  if (pooled) {
+    a.rec_pool.base = (int32_t*)((char*)rec + b_rec + b_n);
+    a.rec_pool.cursor = (unsigned long long*)((char*)rec + b_rec + 2 * b_n);
+    a.rec_pool.cap = b_rec / (sizeof(T) * rl);
+    ikg::poison_int(a.rec_pool.base, sizeof(int32_t) * (size_t)n, s);
+    if (hipMemsetAsync(a.rec_pool.cursor, 0, sizeof(unsigned long long), s) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)ikg::ws_free(&model->ws, rec, s);
+      a.rec = nullptr;
+      a.rec_n = nullptr;
+      a.rec_pool = {};
+      return nullptr;
+    }
+  }
   a.rec_used = rec_used;
   return rec;
 }
@@ -403,6 +432,7 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
     a.rec = tmp.rec;
     a.rec_n = tmp.rec_n;
     a.rec_used = tmp.rec_used;
+    a.rec_pool = tmp.rec_pool;
   }
   e = ikg::launch_multistart<T>(dm, kparams<T>(params), a, model->spec, s);
   if (rec) {
@@ -563,6 +593,24 @@ int ikg_debug_ws_count(const ikg_model* model, int64_t* live, int64_t* pending) 
   std::lock_guard<std::mutex> lock(model->ws.st->mu);
   *live = model->ws.st->live;
   *pending = (int64_t)model->ws.st->pending.size();
+  return IKG_OK;
+}
+
+// Diagnostic (not in include/ikgrasp.h): bytes the model's scratch pools
+// hold from the runtime (reserved) and hand out at the moment (used), summed
+// over devices (hipMemPoolAttrReservedMemCurrent / UsedMemCurrent).
+// tests/test_gpu_memory.py.
+int ikg_debug_ws_pool(const ikg_model* model, int64_t* reserved, int64_t* used) {
+  if (!model || !reserved || !used) return fail(IKG_EINVAL, "bad arguments");
+  *reserved = *used = 0;
+  for (auto& dp : ikg::ws_pools(const_cast<ikg::WsOwner*>(&model->ws), false)) {
+    uint64_t r = 0, u = 0;
+    if (hipMemPoolGetAttribute(dp.second, hipMemPoolAttrReservedMemCurrent, &r) != hipSuccess ||
+        hipMemPoolGetAttribute(dp.second, hipMemPoolAttrUsedMemCurrent, &u) != hipSuccess)
+      return fail(IKG_EHIP, "hipMemPoolGetAttribute failed");
+    *reserved += (int64_t)r;
+    *used += (int64_t)u;
+  }
   return IKG_OK;
 }
 

@@ -32,7 +32,7 @@ __device__ unsigned long long g_cprof[8];
 __device__ unsigned long long g_skip[8];
 // trajectory scan, per problem and window: max / sum of checks, max cycles,
 // sum / max of sweeps, windows scanned, certificates, sum of cycles
-__device__ unsigned long long g_scan[8];
+__device__ unsigned long long g_scan[16];
 #define SKIP_STAT(i, v) atomicAdd(&g_skip[i], (unsigned long long)(v))
 // single-lane witness work: cycles in GJK (pair_collides + supports), in
 // certify_witness (of which EPA), calls of each
@@ -1355,7 +1355,18 @@ struct TrajWs {
   TrajCert<T>* cst;
   int64_t slots;      // slots per parity
   int by_p = 0;       // records, counts and it0 indexed by problem (the pair kernel's records)
+  const int32_t* rbase = nullptr;  // by_p, pooled records: each problem's first record (ikg_solve.hpp RecPool)
+  int cert = 1;       // inscribed-ball certificates before the witness tests (IKG_SCAN_CERT=0: off)
 };
+
+// IKG_SCAN_CERT=0: the records scan without inscribed-ball certificates (A/B knob)
+static int scan_cert() {
+  static const int v = [] {
+    const char* e = getenv("IKG_SCAN_CERT");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
 // the record layout (kRec*, rec_len, store_block8) is in ikg_solve.hpp
 
 template <typename T>
@@ -1556,6 +1567,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
   __shared__ Witness<T> W;
   __shared__ T PL[64][2][12];  // per-lane witness placements
   __shared__ int32_t SL[kMaxNq];  // joint -> record slot
+  __shared__ BallCert<T> BC;   // the witness pair's inscribed-ball certificate (ball_cert)
   const int lane = threadIdx.x;
   const int nq = m->nq, RL = rec_len(m->n_passive);
   const int64_t par = (int64_t)(round & 1) * w.slots;
@@ -1590,10 +1602,16 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     }
     const int64_t ix = w.by_p ? p : par + i;
     const int nr = w.nrec[ix];
+    // the record pool was full when it converged: the trajectory kernel takes it
+    // (launch_collide_continue); wave-uniform
+    if (nr & kTrajNoRec) {
+      __syncthreads();
+      continue;
+    }
     const int nrec = nr & ~kTrajEnded;
     const bool ended = (nr & kTrajEnded) != 0;
     const int it0 = w.it0[ix];
-    T* rec = w.rec + ix * Wn * RL;
+    T* rec = w.rec + (w.rbase ? (int64_t)w.rbase[p] * RL : ix * Wn * RL);
     if (w.by_p) {  // the pair kernel records no passive joints: constant from the first update on
       const T* qo = q_out + p * nq;
       for (int j = lane; j < nrec; j += 64)
@@ -1615,6 +1633,31 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       const int j = start + lane;
       const T* r = rec + (int64_t)min(j, nrec - 1) * RL;
       bool need = j < nrec && r[kRecPass] != T(0);
+      // inscribed-ball certificates of the witness at the chunk's first unproved
+      // record (one lane's placements, ball_cert), then every lane's motion
+      // bound against it (ball_covers): the records it proves need no narrow
+      // phase.  At most two per chunk; what they leave goes to the witness tests.
+      for (int cr = 0; w.cert && cr < 2 && W.pair >= 0; ++cr) {
+        const unsigned long long bn = __ballot(need);
+        if (!bn) break;
+        const int f = start + __ffsll((long long)bn) - 1;
+        if (lane == 0) ball_cert(m, c, W.pair, rec + (int64_t)f * RL, SL, tgt, BC);
+        __syncthreads();
+        const bool ok = BC.r > T(0);
+        const bool cov = ok && need && j >= f && ball_covers(BC, r, SL);
+#ifdef IKG_CPROF
+        if (lane == 0) {
+          atomicAdd(&g_scan[8], 1ull);
+          atomicAdd(&g_scan[9], ok ? 1ull : 0ull);
+          atomicAdd(&g_scan[10], (unsigned long long)__popcll(__ballot(need)));
+        }
+        const unsigned long long nc = __popcll(__ballot(cov));
+        if (lane == 0) atomicAdd(&g_scan[11], nc);
+#endif
+        need = need && !cov;
+        __syncthreads();  // BC is rewritten by the next round
+        if (!ok) break;
+      }
       while (__any(need)) {
         const int wp = W.pair;
         const bool hit = need && wp >= 0 && witness_hit_lane(m, c, wp, r, SL, tgt, PL[lane]);
@@ -1881,6 +1924,7 @@ static hipError_t launch_traj_t(const KModel<T>* dm, const KCollision<T>* dc, co
   w.done = (int32_t*)c, c += b_i;
   w.cst = (TrajCert<T>*)c;
   w.slots = (int64_t)B;
+  w.cert = scan_cert();
   ws_trace("alloc traj", ws, b_rec + b_q + 6 * b_i + b_c, s);
   poison_float(w.rec, b_rec + b_q, s);  // records, qrun
   poison_int(w.itrun, 6 * b_i + b_c, s);  // itrun, it0, nrec, done, cst
@@ -1913,6 +1957,16 @@ static hipError_t launch_traj_t(const KModel<T>* dm, const KCollision<T>* dc, co
   return e != hipSuccess ? e : ef;
 }
 
+
+// Pooled records: the problems the pre-screen left colliding whose record
+// reservation found the pool full (kTrajNoRec) -- listed for the trajectory
+// continuation (marker >= 0: the pre-screen's witness)
+__global__ __launch_bounds__(256) void ikg_mark_norec_kernel(const int32_t* __restrict__ wit,
+                                                             const int32_t* __restrict__ nrec, int64_t B,
+                                                             int32_t* __restrict__ mark) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < B) mark[i] = (wit[i] >= 0 && (nrec[i] & kTrajNoRec)) ? wit[i] : -1;
+}
 
 // listed for the trajectory continuation without a pre-screen: every problem
 // whose errors passed in the batch kernel (marker >= 0 for the compaction)
@@ -1990,6 +2044,8 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     tw.cst = (TrajCert<T>*)(dws + ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255));
     tw.slots = a.B;
     tw.by_p = 1;
+    tw.cert = scan_cert();
+    tw.rbase = a.rec_pool.base;
     ws_trace("alloc scan", dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     poison_int(dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     // one scan round with the pre-screen's witnesses: `done` is only written
@@ -2002,6 +2058,29 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     ws_trace("free scan", dws, 0, s);
     const hipError_t ef2 = ws_free(a.ws_owner, dws, s);
     if (ec == hipSuccess) ec = ef2;
+    if (ec == hipSuccess && a.rec_pool.cursor) {
+      // pooled records: the colliding problems that found the pool full go
+      // through the interleaved continuation, which needs no record buffers
+      // (the list is empty in the usual case, and the launch's waves then
+      // return at once)
+      const size_t b3 = 3 * ib + 256;
+      char* fws = nullptr;
+      ec = ws_alloc(a.ws_owner, (void**)&fws, b3, s);
+      if (ec != hipSuccess) return ec;
+      poison_int(fws, b3, s);
+      ContWs<T> w2{(int32_t*)w.wit, (int32_t*)fws, (int32_t*)(fws + 3 * ib), (int32_t*)(fws + 2 * ib), w.rec};
+      int32_t* mark = (int32_t*)(fws + ib);
+      hipLaunchKernelGGL(ikg_mark_norec_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s,
+                         (const int32_t*)w.wit, (const int32_t*)a.rec_n, a.B, mark);
+      const unsigned nb = (unsigned)((a.B + kCompactChunk - 1) / kCompactChunk);
+      hipLaunchKernelGGL(ikg_compact_count_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)mark, a.B, w2.list);
+      hipLaunchKernelGGL(ikg_compact_write_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)mark, a.B,
+                         (const int32_t*)w2.list, w2.clist, w2.count + 1);
+      launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, nq, ng, w2, s);
+      ec = hipGetLastError();
+      const hipError_t ef3 = ws_free(a.ws_owner, fws, s);
+      if (ec == hipSuccess) ec = ef3;
+    }
   } else if (spec == kSpecNextage) {
     if (damped)
       launch_continue_sel<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, w, s, ec, first);
@@ -2040,7 +2119,7 @@ extern "C" int ikg_debug_wprof(unsigned long long* out, int reset) {
 extern "C" int ikg_debug_scan(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_scan), sizeof(g_scan)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[8] = {};
+    unsigned long long z[16] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_scan), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

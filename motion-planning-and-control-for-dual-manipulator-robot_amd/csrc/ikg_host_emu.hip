@@ -265,6 +265,36 @@ extern "C" int ikg_emu_collision(const ikg_model_desc* d, const ikg_collision_de
   return 0;
 }
 
+// Inscribed-ball certificate of scene pair `pair` at configuration qc (joint
+// order = q order) with the cube at `target` (ball_cert, the records scan's
+// certificate), then whether it proves the pair intersecting at each of the B
+// configurations q (ball_covers).  tests/test_collision.py.
+template <typename T>
+void emu_ball(const ikg_model_desc* d, const ikg_collision_desc* cd, int pair, const void* qc, const void* target,
+              const void* q, int64_t B, double* r_out, uint8_t* covered) {
+  ikg::KModel<T> m;
+  ikg::build_kmodel<T>(*d, m);
+  static thread_local ikg::KCollision<T> kc;
+  ikg::build_kcollision<T>(*cd, kc);
+  int32_t sl[ikg::kMaxNq];
+  for (int k = 0; k < ikg::kMaxNq; ++k) sl[k] = k;
+  static thread_local ikg::BallCert<T> bc;
+  ikg::ball_cert(&m, &kc, pair, (const T*)qc, sl, (const T*)target, bc);
+  *r_out = (double)bc.r;
+  for (int64_t i = 0; i < B; ++i) covered[i] = ikg::ball_covers(bc, (const T*)q + d->nq * i, sl) ? 1 : 0;
+}
+
+extern "C" int ikg_emu_ball_cert(const ikg_model_desc* d, const ikg_collision_desc* cd, int dtype, int pair,
+                                 const void* qc, const void* target, const void* q, int64_t B, double* r_out,
+                                 uint8_t* covered) {
+  if (pair < 0 || pair >= cd->n_pairs) return -1;
+  if (dtype == IKG_F64)
+    emu_ball<double>(d, cd, pair, qc, target, q, B, r_out, covered);
+  else
+    emu_ball<float>(d, cd, pair, qc, target, q, B, r_out, covered);
+  return 0;
+}
+
 // EPA depth certificate of one shape pair (tests/test_collision_epa.py):
 // kinds/placements/dims per ikg_collision_desc conventions; returns
 // pair_collides' verdict in *r and the certified depth bound in *depth (0 when

@@ -59,12 +59,12 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             uint8_t* __restrict__ conv_out,
                                                             int32_t* __restrict__ iters_out,
                                                             T* __restrict__ err_out, T* __restrict__ rec = nullptr,
-                                                            int32_t* __restrict__ rec_n = nullptr) {
+                                                            int32_t* __restrict__ rec_n = nullptr, RecPool pool = {}) {
   // model tables stay in global memory: the compiler hoists them into
   // registers (staging them in LDS and re-reading per iteration measured 8%
   // slower)
   pair_batch_body<T, DAMPED, SP, MED, REC>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
-                                           err_out, rec, rec_n);
+                                           err_out, rec, rec_n, pool);
 }
 
 
@@ -227,11 +227,11 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
       if (med)
         hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, true, true>), grid, dim3(64), lds_pad_bytes(), s,
                            dmodel, prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw,
-                           (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n);
+                           (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n, a.rec_pool);
       else
         hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, false, true>), grid, dim3(64), lds_pad_bytes(), s,
                            dmodel, prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw,
-                           (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n);
+                           (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n, a.rec_pool);
       if (a.rec_used) *a.rec_used = true;
       return;
     }
@@ -356,6 +356,7 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   b.jit = a.jit;
   b.rec = a.rec;
   b.rec_n = a.rec_n;
+  b.rec_pool = a.rec_pool;
   b.rec_used = a.rec_used;
   // AUTO keeps the pair layout here: seeds spread the update counts, and a
   // wave lasts as long as its slowest problem -- 64 per packed wave against 32

@@ -13,6 +13,7 @@
 
 #include "ikg_collision.hpp"
 #include "ikg_device.hpp"
+#include "ikg_solve.hpp"
 
 namespace ikg {
 
@@ -270,6 +271,7 @@ struct BatchArgs {
   void* rec = nullptr;
   int32_t* rec_n = nullptr;
   bool* rec_used = nullptr;
+  RecPool rec_pool = {};        // pooled records (ikg_solve.hpp RecPool), cursor null: fixed slots
   WsOwner* ws_owner = nullptr;  // scratch of captured solves (ws_alloc)
 };
 
@@ -300,6 +302,7 @@ struct MultiArgs {
   void* rec = nullptr;
   int32_t* rec_n = nullptr;
   bool* rec_used = nullptr;
+  RecPool rec_pool = {};
 };
 
 // Debug knob IKG_POISON=1 (read per call): every stream-ordered workspace is

@@ -42,7 +42,7 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               uint8_t* __restrict__ conv_out,
                                                               int32_t* __restrict__ iters_out,
                                                               float* __restrict__ err_out, float* __restrict__ rec = nullptr,
-                                                              int32_t* __restrict__ rec_n = nullptr) {
+                                                              int32_t* __restrict__ rec_n = nullptr, RecPool pool = {}) {
   if constexpr (WPS == 1) asm volatile("" ::: "a255");
   // v171: at least 172 VGPRs, so 2 waves fit and 3 do not; an AGPR claim
   // instead makes the allocator split the 2-wave budget 128 VGPR / 128 AGPR
@@ -63,11 +63,15 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
   v2f nrm, other;
   if constexpr (REC) {
     const int rl = rec_len(m->n_passive);
-    const RecOut<float> ro{rec + p * (int64_t)(prm.max_iters + 1) * rl, rec_n + p, qrow, q_out + p * m->nq,
-                           conv_out + p, iters_out + p, err_out + p * 2, rl};
+    RecOut<float> ro{pool.cursor ? rec : rec + p * (int64_t)(prm.max_iters + 1) * rl, rec_n + p, qrow,
+                     q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl};
+    if (pool.cursor) {
+      ro.pool = pool;
+      ro.pool.base = pool.base + p;
+      pool.base[p] = -1;
+    }
     rec_n[p] = 0;
-    solve_pair<v2f, false, SP, MED, true>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro);
-    if (conv) return;
+    if (solve_pair<v2f, false, SP, MED, true>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
     solve_pair<v2f, false, SP, MED>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
   }
@@ -144,7 +148,7 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(64), packed_lds_pad(), s, dmodel, prm, (const float*)a.targets,
                        (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out, a.converged, a.iters,
-                       (float*)a.err_out, (float*)a.rec, a.rec_n);
+                       (float*)a.err_out, (float*)a.rec, a.rec_n, a.rec_pool);
   };
 #ifndef IKG_PACKED_REC
 #define IKG_PACKED_REC 1

@@ -257,3 +257,54 @@ def test_scene_json_roundtrip():
     from ikgrasp.collision import CollisionScene
     again = CollisionScene.from_json(ps.to_json())
     assert json.loads(again.to_json()) == json.loads(ps.to_json())
+
+
+@pytest.mark.parametrize("dtype", [0, 1])
+def test_ball_certificate_is_sound(col_cases, oscene, dtype):
+    """The records scan's inscribed-ball certificate (ikg_collision.hpp
+    ball_cert / ball_covers, run here through the host emulator): at colliding
+    fixture configurations, every colliding pair gets a certificate, and every
+    perturbed configuration it claims still intersects does, by the collision
+    oracle's own narrow phase (oracle/collision_oracle.py collide).  The
+    certificate must also cover most small perturbations (it exists to skip
+    narrow phases)."""
+    lib = C.CDLL(EMU)
+    vp = C.c_void_p
+    lib.ikg_emu_ball_cert.argtypes = [vp, vp, C.c_int, C.c_int, vp, vp, vp, C.c_int64, vp, vp]
+    md = _lib.model_desc(load_nextage())
+    scene = load_nextage_scene()
+    cd = _lib.collision_desc(scene)
+    index = {tuple(p): k for k, p in enumerate(scene.pairs.tolist())}
+    npt = np.float64 if dtype == 0 else np.float32
+    rng = np.random.default_rng(17 + dtype)
+    col = np.nonzero(col_cases["collision"] & col_cases["robust64"])[0]
+    rng.shuffle(col)
+    gs = oscene["geoms"]
+    n_cert = n_pairs = n_cov = n_small = n_small_cov = 0
+    for i in col[:40]:
+        q, tg = col_cases["q"][i], col_cases["targets"][i]
+        TR, Tt = tg[:9].reshape(3, 3), tg[9:]
+        for a, b in co.colliding_pairs(oscene, q, TR, Tt):
+            n_pairs += 1
+            scales = np.repeat([1e-5, 1e-4, 1e-3, 1e-2], 8)
+            dq = rng.uniform(-1, 1, (len(scales), 15)) * scales[:, None]
+            qs = np.ascontiguousarray(q[None] + dq, dtype=npt)
+            r = C.c_double()
+            cov = np.empty(len(qs), np.uint8)
+            qc = np.ascontiguousarray(q, dtype=npt)
+            tgc = np.ascontiguousarray(tg, dtype=npt)
+            assert lib.ikg_emu_ball_cert(C.byref(md), C.byref(cd), dtype, index[(a, b)], qc.ctypes.data,
+                                         tgc.ctypes.data, qs.ctypes.data, len(qs), C.byref(r),
+                                         cov.ctypes.data) == 0
+            if r.value > 0:
+                n_cert += 1
+            n_small += 8
+            n_small_cov += int(cov[:8].sum())
+            for k in np.nonzero(cov)[0]:
+                n_cov += 1
+                P = co.geom_poses(oscene, qs[k].astype(np.float64), TR, Tt)
+                assert co.collide(gs[a], P[a][0], P[a][1], gs[b], P[b][0], P[b][1]), (i, a, b, k, r.value)
+    print(f"dtype {dtype}: {n_pairs} colliding pairs, {n_cert} certified, {n_cov} perturbed configurations "
+          f"proved (all confirmed), 1e-5 perturbations covered {n_small_cov}/{n_small}")
+    assert n_pairs >= 40 and n_cert >= 0.8 * n_pairs
+    assert n_small_cov >= 0.5 * n_small

@@ -381,3 +381,42 @@ def test_poisoned_workspaces_give_the_same_answers(csolver, solve_cases, monkeyp
         assert np.array_equal(sol.converged, ref.converged) and np.array_equal(sol.iters, ref.iters), env
         for k in env:
             monkeypatch.delenv(k)
+
+
+def test_pooled_records_equal_fixed_records(csolver, monkeypatch):
+    """Records beyond the fixed-slot budget come from a pool the converged
+    problems reserve from (ikg_solve.hpp RecPool): C2's 4,096 fp64 targets with
+    a 256 MB budget (pooled, enough room) give the fixed slots' bits; with a
+    4 MB budget most problems find the pool full and go through the
+    trajectory kernel instead: same flags and update counts, q to the
+    trajectory kernel's rounding (1e-9)."""
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(4096, seed=0)
+    a = csolver.solve(tg, np.zeros(15), check_collision=True)  # fixed slots (656 MB)
+    monkeypatch.setenv("IKG_REC_BUDGET_MB", "256")
+    b = csolver.solve(tg, np.zeros(15), check_collision=True)
+    for x, y in zip((a.q, a.converged, a.iters, a.err), (b.q, b.converged, b.iters, b.err)):
+        assert np.array_equal(x, y)
+    monkeypatch.setenv("IKG_REC_BUDGET_MB", "4")
+    c = csolver.solve(tg, np.zeros(15), check_collision=True)
+    assert np.array_equal(a.converged, c.converged) and np.array_equal(a.iters, c.iters)
+    assert np.abs(a.q - c.q).max() <= 1e-9
+
+
+def test_pooled_records_c3_fp32(csolver, monkeypatch):
+    """C3 (65,536 fp32, packed layout) with the collision term: its fixed
+    records (5.2 GB) exceed the budget, so the packed kernel records into the
+    pool; against the trajectory kernel for the whole batch (IKG_REC_POOL=0):
+    flags and counts agree on >= 99.9% (fp32: the trajectory kernel resyncs
+    its trig per window), q to fp32 rounding, deterministic."""
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(65536, seed=0)
+    a = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
+    a2 = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
+    assert np.array_equal(a.q, a2.q) and np.array_equal(a.iters, a2.iters)
+    monkeypatch.setenv("IKG_REC_POOL", "0")
+    b = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
+    same = (a.converged == b.converged) & (a.iters == b.iters)
+    print(f"C3 fp32 pooled records vs trajectory kernel: {int((~same).sum())} of 65536 differ in flag or count")
+    assert same.mean() >= 0.999
+    assert np.abs(a.q[same] - b.q[same]).max() <= 1e-3

@@ -11,7 +11,7 @@ mkdir -p $O
 export IKG_REPORT_DIR=$O/reports
 stop() { case $1 in 0|1) return 0;; *) echo "FATAL $2 rc=$1"; exit $1;; esac; }
 if [ -n "$FIRST" ]; then
-  timeout -k 10 ${FIRST_TIMEOUT:-600} python -u -m pytest $FIRST -m gpu -x -v -s --timeout 300 --timeout-method thread \
+  timeout -k 10 ${FIRST_TIMEOUT:-600} python -u -m pytest $FIRST -m gpu ${XFLAG--x} -v -s --timeout 300 --timeout-method thread \
     > $O/pytest_first.log 2>&1
   rc=$?; echo "first rc=$rc"; grep -E "passed|failed" $O/pytest_first.log | tail -1; stop $rc first
 fi

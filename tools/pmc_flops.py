@@ -13,7 +13,9 @@ Lanes of problems that have already stopped are masked off but still occupy
 the issue slot, so the counts are divided by the wave-iterations the launch
 actually ran: sum over waves of (max updates in the wave + 1 evaluations).
 
-usage: python tools/pmc_flops.py gpurun_out/flops/<dtype>_b<B> B dtype tag"""
+usage: python tools/pmc_flops.py gpurun_out/flops/<dtype>_b<B> B dtype tag [--med]
+--med: the medium-range (per-problem seeds, multi-start) instantiation ->
+profiles/flops_<layout>_<dtype>_med.json (bench.py flops_profile)."""
 import csv
 import json
 import os
@@ -54,12 +56,16 @@ def main(d, B, dtype, tag):
                    f"x {lanes} lane(s)/problem" +
                    ("; v_pk_* instructions counted once (lower bound: each carries both arms)"
                     if short == "packed" else "")}
-    path = os.path.join(ROOT, "profiles", f"flops_{short}_{dtype}.json" if short == "packed" else
-                        f"flops_{dtype}_b{B}.json")
+    med = "--med" in sys.argv
+    if med:
+        out["instantiation"] = "medium-range trig rule (per-problem q0 rows / multi-start seeds)"
+    path = os.path.join(ROOT, "profiles", f"flops_{short}_{dtype}_med.json" if med else
+                        f"flops_{short}_{dtype}.json" if short == "packed" else f"flops_{dtype}_b{B}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(path, out)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4] if len(sys.argv) > 4 else "r03")
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    main(args[0], int(args[1]), args[2], args[3] if len(args) > 3 else "r03")

@@ -48,9 +48,10 @@ def main_collision(pmc_dir, dtype, B, tag, solves):
     print(path, out)
 
 
-def main(pmc_dir, dtype, B, tag):
-    fetch = statistics.median(per_dispatch(os.path.join(pmc_dir, f"fetch_b{B}_{dtype}"), "FETCH_SIZE"))
-    write = statistics.median(per_dispatch(os.path.join(pmc_dir, f"write_b{B}_{dtype}"), "WRITE_SIZE"))
+def main(pmc_dir, dtype, B, tag, sfx=""):
+    x = f"_{sfx}" if sfx else ""
+    fetch = statistics.median(per_dispatch(os.path.join(pmc_dir, f"fetch_b{B}_{dtype}{x}"), "FETCH_SIZE"))
+    write = statistics.median(per_dispatch(os.path.join(pmc_dir, f"write_b{B}_{dtype}{x}"), "WRITE_SIZE"))
     out = {
         "kernel": "ikg_packed_batch_kernel" if (dtype == "f32" and B >= 65536) else "ikg_pair_batch_kernel",
         "dtype": dtype, "batch": B, "round": tag,
@@ -58,7 +59,9 @@ def main(pmc_dir, dtype, B, tag):
         "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
         "note": "2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes; median over dispatches",
     }
-    path = os.path.join(ROOT, "profiles", f"pmc_{dtype}_b{B}.json")
+    if sfx:
+        out["workload"] = sfx
+    path = os.path.join(ROOT, "profiles", f"pmc_{dtype}_b{B}{x}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(path, out)
@@ -68,4 +71,6 @@ if __name__ == "__main__":
     if "--collision" in sys.argv:
         main_collision(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[6]))
         sys.exit(0)
-    main(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4] if len(sys.argv) > 4 else "r01")
+    sfx = next((a[6:] for a in sys.argv if a.startswith("--sfx=")), "")
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    main(args[0], args[1], int(args[2]), args[3] if len(args) > 3 else "r01", sfx)
