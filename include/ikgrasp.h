@@ -71,10 +71,11 @@
  *     synchronisation.  ikg_model_trim synchronises each such device and
  *     releases everything the pools hold unused; ikg_model_destroy
  *     synchronises and destroys the pools.  Released memory goes back to the
- *     HIP runtime, which may keep it mapped for later pools and allocations
- *     of the process (the device's free-memory figure then does not rise);
- *     a destroyed model leaves that figure where it was before the model
- *     existed (tests/test_gpu_memory.py).  IKG_WS_POOL=0 in the environment
+ *     HIP runtime, which keeps it mapped for later pools and allocations of
+ *     the process (the device's free-memory figure does not rise; a second
+ *     model reuses it without taking more of the device), and a destroyed
+ *     model leaves that figure where it was before the model existed
+ *     (tests/test_gpu_memory.py).  IKG_WS_POOL=0 in the environment
  *     selects the device's default pool.
  */
 #ifndef IKGRASP_H

@@ -1568,6 +1568,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
   __shared__ T PL[64][2][12];  // per-lane witness placements
   __shared__ int32_t SL[kMaxNq];  // joint -> record slot
   __shared__ BallCert<T> BC;   // the witness pair's inscribed-ball certificate (ball_cert)
+  __shared__ int32_t bc_pair;  // the pair BC certifies (-1: none yet for this problem)
   const int lane = threadIdx.x;
   const int nq = m->nq, RL = rec_len(m->n_passive);
   const int64_t par = (int64_t)(round & 1) * w.slots;
@@ -1584,6 +1585,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       const int wp0 = round < 0 ? -1 : (witness0 && round == 0) ? witness0[p] : w.cst[i].pair;
       W.pair = wp0 >= 0 && wp0 < c->n_pairs ? wp0 : -1;  // a witness is only a hint: never trust an index
       W.cert_ok = 0;
+      bc_pair = -1;
     }
     if (round < 0 && lane < nq) S.q[lane] = q_out[p * nq + lane];
     __syncthreads();
@@ -1633,30 +1635,39 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       const int j = start + lane;
       const T* r = rec + (int64_t)min(j, nrec - 1) * RL;
       bool need = j < nrec && r[kRecPass] != T(0);
-      // inscribed-ball certificates of the witness at the chunk's first unproved
-      // record (one lane's placements, ball_cert), then every lane's motion
-      // bound against it (ball_covers): the records it proves need no narrow
-      // phase.  At most two per chunk; what they leave goes to the witness tests.
-      for (int cr = 0; w.cert && cr < 2 && W.pair >= 0; ++cr) {
-        const unsigned long long bn = __ballot(need);
-        if (!bn) break;
-        const int f = start + __ffsll((long long)bn) - 1;
-        if (lane == 0) ball_cert(m, c, W.pair, rec + (int64_t)f * RL, SL, tgt, BC);
-        __syncthreads();
-        const bool ok = BC.r > T(0);
-        const bool cov = ok && need && j >= f && ball_covers(BC, r, SL);
+      // inscribed-ball certificates of the witness pair: every lane's motion
+      // bound against the current certificate (ball_covers) proves its record
+      // colliding with no narrow phase; a new certificate (one lane's
+      // placements and point search, ball_cert) at the first record left
+      // unproved, at most two per chunk; what they leave goes to the witness
+      // tests.  A certificate carries over to the next chunk while its pair
+      // stays the witness.
+      for (int cr = 0; w.cert && W.pair >= 0; ++cr) {
+        if (bc_pair == W.pair) {  // wave-uniform (LDS)
+          const bool cov = need && ball_covers(BC, r, SL);
 #ifdef IKG_CPROF
-        if (lane == 0) {
-          atomicAdd(&g_scan[8], 1ull);
-          atomicAdd(&g_scan[9], ok ? 1ull : 0ull);
-          atomicAdd(&g_scan[10], (unsigned long long)__popcll(__ballot(need)));
-        }
-        const unsigned long long nc = __popcll(__ballot(cov));
-        if (lane == 0) atomicAdd(&g_scan[11], nc);
+          const unsigned long long nn = __popcll(__ballot(need)), nc = __popcll(__ballot(cov));
+          if (lane == 0) {
+            atomicAdd(&g_scan[10], nn);
+            atomicAdd(&g_scan[11], nc);
+          }
 #endif
-        need = need && !cov;
-        __syncthreads();  // BC is rewritten by the next round
-        if (!ok) break;
+          need = need && !cov;
+        }
+        const unsigned long long bn = __ballot(need);
+        if (!bn || cr == 2) break;
+        const int f = start + __ffsll((long long)bn) - 1;
+        __syncthreads();  // every lane has read BC
+        if (lane == 0) {
+          ball_cert(m, c, W.pair, rec + (int64_t)f * RL, SL, tgt, BC);
+          bc_pair = BC.r > T(0) ? W.pair : -1;
+#ifdef IKG_CPROF
+          atomicAdd(&g_scan[8], 1ull);
+          atomicAdd(&g_scan[9], BC.r > T(0) ? 1ull : 0ull);
+#endif
+        }
+        __syncthreads();
+        if (bc_pair < 0) break;
       }
       while (__any(need)) {
         const int wp = W.pair;

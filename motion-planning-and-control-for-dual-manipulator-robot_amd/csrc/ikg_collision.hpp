@@ -920,67 +920,90 @@ IKG_HD inline void shape_constraints(const Shape<T>& s, const T* x, T (&c)[6], T
   }
 }
 
-// A point deep inside both shapes and the radius of the ball around it that
-// lies in both (<= 0: none found): the Chebyshev centre of A n B, approached
-// by ascent on a soft minimum of the two shapes' constraints (weights
-// exp(-(c_k - min)/tau), the softness and the step shrinking geometrically)
-// from the best of the two centres, their midpoint and the point between the
-// closest points of the two cores where the cores' depth estimates meet.  The
-// depth of every visited point is evaluated exactly and the deepest is kept,
-// so the search only decides how large the certified radius is, never
-// whether it holds (on random colliding fixture poses it finds a positive
-// radius for ~97% of the colliding pairs; a full optimiser: all of them).
-template <typename T>
-IKG_HD inline T deep_common_point(const Shape<T>& A, const Shape<T>& B, T* p) {
-  T a0[3], a1[3], b0[3], b1[3], ra, rb, s[3], t[3];
+// A point deep inside both shapes (the search for deep_common_point, in fp32
+// whatever the solve's type: it only has to find a good point): the Chebyshev
+// centre of A n B, approached by ascent on a soft minimum of the two shapes'
+// constraints (weights max(0, 1 - (c_k - min)/tau)^2 -- no transcendental --
+// with the softness and the step shrinking geometrically) from the best of
+// the two centres, their midpoint and the point between the closest points of
+// the two cores where the cores' depth estimates meet.
+IKG_HD inline void deep_point_search(const Shape<float>& A, const Shape<float>& B, float* p) {
+  float a0[3], a1[3], b0[3], b1[3], ra, rb, s[3], t[3];
   shape_core(A, a0, a1, ra);
   shape_core(B, b0, b1, rb);
   closest_segments(a0, a1, b0, b1, s, t);
-  T D = T(0);
+  float D = 0.f;
   for (int i = 0; i < 3; ++i) D += (t[i] - s[i]) * (t[i] - s[i]);
-  D = sqrt(D);
-  const T fm = D > T(0) ? fmin(fmax((D + ra - rb) / (T(2) * D), T(0)), T(1)) : T(0.5);
-  T best = T(-1e30);
+  D = sqrtf(D);
+  const float fm = D > 0.f ? fminf(fmaxf((D + ra - rb) / (2.f * D), 0.f), 1.f) : 0.5f;
+  float best = -1e30f;
   for (int cnd = 0; cnd < 4; ++cnd) {
-    T x[3];
+    float x[3];
     for (int i = 0; i < 3; ++i)
-      x[i] = cnd == 0 ? s[i] + fm * (t[i] - s[i]) : cnd == 1 ? A.t[i] : cnd == 2 ? B.t[i] : T(0.5) * (A.t[i] + B.t[i]);
-    const T r = fmin(shape_depth(A, x), shape_depth(B, x));
+      x[i] = cnd == 0 ? s[i] + fm * (t[i] - s[i]) : cnd == 1 ? A.t[i] : cnd == 2 ? B.t[i] : 0.5f * (A.t[i] + B.t[i]);
+    const float r = fminf(shape_depth(A, x), shape_depth(B, x));
     if (r > best) {
       best = r;
       for (int i = 0; i < 3; ++i) p[i] = x[i];
     }
   }
-  T scale = T(0);
-  for (int i = 0; i < 3; ++i) scale = fmax(scale, fmax(A.dims[i], B.dims[i]));
-  T x[3] = {p[0], p[1], p[2]};
-  T tau = T(0.2) * scale, eta = T(0.5) * scale;
+  float scale = 0.f;
+  for (int i = 0; i < 3; ++i) scale = fmaxf(scale, fmaxf(A.dims[i], B.dims[i]));
+  float x[3] = {p[0], p[1], p[2]};
+  float tau = 0.2f * scale, eta = 0.5f * scale;
   for (int it = 0; it < IKG_DEEP_ITERS; ++it) {
-    T ca[6], ga[6][3], cb[6], gb[6][3];
+    float ca[6], ga[6][3], cb[6], gb[6][3];
     shape_constraints(A, x, ca, ga);
     shape_constraints(B, x, cb, gb);
-    T m = ca[0];
+    float m = ca[0];
 #pragma unroll
-    for (int k = 0; k < 6; ++k) m = fmin(m, fmin(ca[k], cb[k]));
+    for (int k = 0; k < 6; ++k) m = fminf(m, fminf(ca[k], cb[k]));
     if (m > best) {
       best = m;
       for (int i = 0; i < 3; ++i) p[i] = x[i];
     }
-    const T itau = T(1) / (tau + T(1e-7));
-    T u[3] = {T(0), T(0), T(0)}, wsum = T(0);
+    const float itau = 1.f / tau;
+    float u[3] = {0.f, 0.f, 0.f}, wsum = 0.f;
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
-      const T wa = exp(fmax((m - ca[k]) * itau, T(-60))), wb = exp(fmax((m - cb[k]) * itau, T(-60)));
+      float wa = fmaxf(1.f - (ca[k] - m) * itau, 0.f), wb = fmaxf(1.f - (cb[k] - m) * itau, 0.f);
+      wa *= wa;
+      wb *= wb;
       wsum += wa + wb;
 #pragma unroll
       for (int i = 0; i < 3; ++i) u[i] += wa * ga[k][i] + wb * gb[k][i];
     }
-    const T f = eta / wsum;
+    const float f = eta / wsum;  // wsum >= 1: the binding constraint weighs 1
     for (int i = 0; i < 3; ++i) x[i] += f * u[i];
-    tau *= T(0.7);
-    eta *= T(0.8);
+    tau *= 0.7f;
+    eta *= 0.8f;
   }
-  return best;
+}
+
+// A point deep inside both shapes and the radius of the ball around it that
+// lies in both (<= 0: none found).  The point comes from the fp32 search
+// above; its depth is evaluated exactly in the solve's type, so the search
+// only decides how large the certified radius is, never whether it holds (on
+// random colliding fixture poses it finds a positive radius for ~97% of the
+// colliding pairs; a full optimiser: all of them).
+template <typename T>
+IKG_HD inline T deep_common_point(const Shape<T>& A, const Shape<T>& B, T* p) {
+  float RA[9], tA[3], dA[3], RB[9], tB[3], dB[3];
+  for (int i = 0; i < 9; ++i) {
+    RA[i] = (float)A.R[i];
+    RB[i] = (float)B.R[i];
+  }
+  for (int i = 0; i < 3; ++i) {
+    tA[i] = (float)A.t[i];
+    tB[i] = (float)B.t[i];
+    dA[i] = (float)A.dims[i];
+    dB[i] = (float)B.dims[i];
+  }
+  const Shape<float> Af{RA, tA, dA, A.kind}, Bf{RB, tB, dB, B.kind};
+  float pf[3];
+  deep_point_search(Af, Bf, pf);
+  for (int i = 0; i < 3; ++i) p[i] = T(pf[i]);
+  return fmin(shape_depth(A, p), shape_depth(B, p));
 }
 
 // Certificate of one pair at one iterate: the joints below the pair's common
