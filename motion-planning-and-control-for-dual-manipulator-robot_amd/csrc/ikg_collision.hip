@@ -32,7 +32,7 @@ __device__ unsigned long long g_cprof[8];
 __device__ unsigned long long g_skip[8];
 // trajectory scan, per problem and window: max / sum of checks, max cycles,
 // sum / max of sweeps, windows scanned, certificates, sum of cycles
-__device__ unsigned long long g_scan[16];
+__device__ unsigned long long g_scan[24];
 #define SKIP_STAT(i, v) atomicAdd(&g_skip[i], (unsigned long long)(v))
 // single-lane witness work: cycles in GJK (pair_collides + supports), in
 // certify_witness (of which EPA), calls of each
@@ -1359,13 +1359,12 @@ struct TrajWs {
   int cert = 1;       // inscribed-ball certificates before the witness tests (IKG_SCAN_CERT=0: off)
 };
 
-// IKG_SCAN_CERT=0: the records scan without inscribed-ball certificates (A/B knob)
+// IKG_SCAN_CERT=0: the records scan without inscribed-ball certificates (A/B
+// knob, read at every launch so one process can compare both: the answers do
+// not depend on it, tests/test_gpu_collision.py)
 static int scan_cert() {
-  static const int v = [] {
-    const char* e = getenv("IKG_SCAN_CERT");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
+  const char* e = getenv("IKG_SCAN_CERT");
+  return e ? atoi(e) : 1;
 }
 // the record layout (kRec*, rec_len, store_block8) is in ikg_solve.hpp
 
@@ -1555,6 +1554,58 @@ __device__ inline bool witness_hit_lane(const KModel<T>* __restrict__ m, const K
 // round = -1 (no pre-screen): the first check of every listed problem, at the
 // iterate the batch kernel stopped at (q_out): collision-free problems are
 // final there, the others get their first witness.
+// ball_cert over the wave: lane 0 walks the chains, the lanes place a joint
+// each, lane 0 composes, then every lane runs the point search from its own
+// start (deep_point_from) and the deepest point (lowest start on a tie, as
+// deep_common_point) is the certificate's.  Wave-uniform; ends synchronised.
+template <typename T>
+__device__ inline void scan_ball_cert(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c, int pair,
+                                      const T* __restrict__ q, const int32_t* sl, const int32_t* par, const T* tgt,
+                                      BallCert<T>& bc, T (*Lt)[12], unsigned long long* pc = nullptr) {
+  const int lane = threadIdx.x;
+#ifdef IKG_CPROF
+  const unsigned long long c0 = clock64();
+#endif
+  if (lane == 0) cert_chains(c, par, pair, bc);
+  __syncthreads();
+  const int ne = bc.nl[0] + bc.nl[1] + bc.nl[2];
+  for (int e = lane; e < ne; e += 64) cert_local(m, q, sl, e, bc, Lt);
+  __syncthreads();
+  if (lane == 0) cert_compose(c, q, sl, tgt, bc, Lt);
+  __syncthreads();
+#ifdef IKG_CPROF
+  const unsigned long long c1 = clock64();
+#endif
+  T PA[12], PB[12], x[3];
+  Shape<T> A{}, B{};
+  cert_shapes(c, bc, PA, PB, A, B);
+  static_assert(kCertStarts == 64, "one start per lane");
+  const T r = deep_point_depth(A, B, lane, x);
+  T best = r;
+  int bl = lane;
+  for (int o = 32; o > 0; o >>= 1) {
+    const T ob = __shfl_xor(best, o);
+    const int ol = __shfl_xor(bl, o);
+    if (ob > best || (ob == best && ol < bl)) {
+      best = ob;
+      bl = ol;
+    }
+  }
+#ifdef IKG_CPROF
+  const unsigned long long c2 = clock64();
+#endif
+  __syncthreads();  // every lane has read the placements
+  if (lane == bl) cert_finish(r, x, bc);
+  __syncthreads();
+#ifdef IKG_CPROF
+  if (pc) {  // cycles: placements, point search, radius and levers (the caller's per-window counters)
+    pc[4] += c1 - c0;
+    pc[5] += c2 - c1;
+    pc[6] += clock64() - c2;
+  }
+#endif
+}
+
 template <typename T>
 __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
                                                const T* __restrict__ targets, int64_t S_per_target,
@@ -1569,6 +1620,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
   __shared__ int32_t SL[kMaxNq];  // joint -> record slot
   __shared__ BallCert<T> BC;   // the witness pair's inscribed-ball certificate (ball_cert)
   __shared__ int32_t bc_pair;  // the pair BC certifies (-1: none yet for this problem)
+  __shared__ int32_t bc_fail;  // a pair whose certificate came out empty: not tried again for this problem
   const int lane = threadIdx.x;
   const int nq = m->nq, RL = rec_len(m->n_passive);
   const int64_t par = (int64_t)(round & 1) * w.slots;
@@ -1586,6 +1638,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       W.pair = wp0 >= 0 && wp0 < c->n_pairs ? wp0 : -1;  // a witness is only a hint: never trust an index
       W.cert_ok = 0;
       bc_pair = -1;
+      bc_fail = -1;
     }
     if (round < 0 && lane < nq) S.q[lane] = q_out[p * nq + lane];
     __syncthreads();
@@ -1614,6 +1667,16 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     const bool ended = (nr & kTrajEnded) != 0;
     const int it0 = w.it0[ix];
     T* rec = w.rec + (w.rbase ? (int64_t)w.rbase[p] * RL : ix * Wn * RL);
+#ifdef IKG_CPROF
+    // per-window counters, flushed once at the window's end (atomics inside the
+    // loop would make the next load wait on them): 0 certificates, 1 positive,
+    // 2 records tested against one, 3 proved, 4-6 certificate cycles, 7 cover
+    // cycles, 8 cover calls, 9 chunk stage cycles, 10 witness cycles, 11 passive fill
+    unsigned long long pc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    const unsigned long long cp0 = clock64();
+#else
+    unsigned long long* pc = nullptr;
+#endif
     if (w.by_p) {  // the pair kernel records no passive joints: constant from the first update on
       const T* qo = q_out + p * nq;
       for (int j = lane; j < nrec; j += 64)
@@ -1631,7 +1694,13 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
 #else
     unsigned long long* prof = nullptr;
 #endif
+#ifdef IKG_CPROF
+    pc[11] += clock64() - cp0;  // passive columns
+#endif
     for (int start = 0; start < nrec && ans < 0; start += 64) {
+#ifdef IKG_CPROF
+      const unsigned long long cc0 = clock64();
+#endif
       const int j = start + lane;
       const T* r = rec + (int64_t)min(j, nrec - 1) * RL;
       bool need = j < nrec && r[kRecPass] != T(0);
@@ -1639,36 +1708,55 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       // bound against the current certificate (ball_covers) proves its record
       // colliding with no narrow phase; a new certificate (one lane's
       // placements and point search, ball_cert) at the first record left
-      // unproved, at most two per chunk; what they leave goes to the witness
+      // unproved, at most one per chunk; what they leave goes to the witness
       // tests.  A certificate carries over to the next chunk while its pair
-      // stays the witness.
-      for (int cr = 0; w.cert && W.pair >= 0; ++cr) {
+      // stays the witness.  It costs about a witness round and a half, so it
+      // pays only when it proves most of a chunk: a pair whose new certificate
+      // comes out empty (it barely intersects) or proves fewer than
+      // kCertYield of the chunk's records is left to the witness tests for the
+      // rest of the window.
+      constexpr int kCertYield = 32;
+      int n_before = 0;
+      for (int cr = 0; w.cert && W.pair >= 0 && W.pair != bc_fail; ++cr) {
         if (bc_pair == W.pair) {  // wave-uniform (LDS)
-          const bool cov = need && ball_covers(BC, r, SL);
+#ifdef IKG_CPROF
+          const unsigned long long cv0 = clock64();
+#endif
+          const bool cov = need && ball_covers(BC, r);
 #ifdef IKG_CPROF
           const unsigned long long nn = __popcll(__ballot(need)), nc = __popcll(__ballot(cov));
-          if (lane == 0) {
-            atomicAdd(&g_scan[10], nn);
-            atomicAdd(&g_scan[11], nc);
-          }
+          pc[7] += clock64() - cv0;
+          pc[8] += 1;
+          pc[2] += nn;
+          pc[3] += nc;
 #endif
           need = need && !cov;
         }
         const unsigned long long bn = __ballot(need);
-        if (!bn || cr == 2) break;
+        if (cr == 1) {  // the new certificate's yield
+          if (lane == 0 && n_before - __popcll(bn) < kCertYield) bc_fail = W.pair;
+          __syncthreads();
+        }
+        if (!bn || cr == 1) break;
+        n_before = __popcll(bn);
         const int f = start + __ffsll((long long)bn) - 1;
         __syncthreads();  // every lane has read BC
+        scan_ball_cert(m, c, W.pair, rec + (int64_t)f * RL, SL, S.par, tgt, BC, S.L, pc);  // S.L: free between full checks
         if (lane == 0) {
-          ball_cert(m, c, W.pair, rec + (int64_t)f * RL, SL, tgt, BC);
           bc_pair = BC.r > T(0) ? W.pair : -1;
-#ifdef IKG_CPROF
-          atomicAdd(&g_scan[8], 1ull);
-          atomicAdd(&g_scan[9], BC.r > T(0) ? 1ull : 0ull);
-#endif
+          if (bc_pair < 0) bc_fail = W.pair;
         }
+#ifdef IKG_CPROF
+        pc[0] += 1;
+        pc[1] += BC.r > T(0) ? 1 : 0;
+#endif
         __syncthreads();
         if (bc_pair < 0) break;
       }
+#ifdef IKG_CPROF
+      const unsigned long long cw = clock64();
+      pc[9] += cw - cc0;  // record reads, covers and certificates
+#endif
       while (__any(need)) {
         const int wp = W.pair;
         const bool hit = need && wp >= 0 && witness_hit_lane(m, c, wp, r, SL, tgt, PL[lane]);
@@ -1693,6 +1781,9 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
         __syncthreads();
         need = need && !hit && j > f;  // unproved records after f: try the new witness
       }
+#ifdef IKG_CPROF
+      pc[10] += clock64() - cw;  // witness rounds and full checks
+#endif
     }
 #ifdef IKG_CPROF
     if (lane == 0) {
@@ -1705,6 +1796,9 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       atomicAdd(&g_scan[5], 1ull);
       atomicAdd(&g_scan[6], n_lane);
       atomicAdd(&g_scan[7], cyc);
+      const int map[12] = {8, 9, 10, 11, 12, 13, 14, 18, 19, 16, 15, 17};
+#pragma unroll
+      for (int k = 0; k < 12; ++k) atomicAdd(&g_scan[map[k]], pc[k]);
     }
 #endif
     const int a = ans >= 0 ? ans : (ended ? nrec - 1 : -1);
@@ -1749,8 +1843,11 @@ void ikg_traj_update_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                              (int)gridDim.x);
 }
 
+// fp32: at most 168 VGPRs, so 3 waves fit a SIMD as before the certificate
+// code (which alone would take the kernel to 182 and 2 waves)
 template <typename T>
-__global__ __launch_bounds__(64) void ikg_traj_scan_kernel(const KModel<T>* __restrict__ m,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 3 : 1)))
+void ikg_traj_scan_kernel(const KModel<T>* __restrict__ m,
                                                            const KCollision<T>* __restrict__ c,
                                                            const T* __restrict__ targets, int64_t S_per_target,
                                                            const int32_t* __restrict__ clist,
@@ -2130,7 +2227,7 @@ extern "C" int ikg_debug_wprof(unsigned long long* out, int reset) {
 extern "C" int ikg_debug_scan(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_scan), sizeof(g_scan)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[24] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_scan), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

@@ -17,9 +17,6 @@ namespace ikg {
 constexpr int kMaxGeoms = 64;
 constexpr int kMaxPairs = 1024;
 constexpr int kGjkIters = 48;
-#ifndef IKG_DEEP_ITERS
-#define IKG_DEEP_ITERS 24
-#endif
 
 enum { kSphere = 0, kBox = 1, kCylinder = 2, kMeshBox = 3 };
 
@@ -920,14 +917,20 @@ IKG_HD inline void shape_constraints(const Shape<T>& s, const T* x, T (&c)[6], T
   }
 }
 
-// A point deep inside both shapes (the search for deep_common_point, in fp32
-// whatever the solve's type: it only has to find a good point): the Chebyshev
-// centre of A n B, approached by ascent on a soft minimum of the two shapes'
-// constraints (weights max(0, 1 - (c_k - min)/tau)^2 -- no transcendental --
-// with the softness and the step shrinking geometrically) from the best of
-// the two centres, their midpoint and the point between the closest points of
-// the two cores where the cores' depth estimates meet.
-IKG_HD inline void deep_point_search(const Shape<float>& A, const Shape<float>& B, float* p) {
+// Certificate point search, in fp32 whatever the solve's type (it only has to
+// find a good point; its depth is then evaluated exactly): ascent on a soft
+// minimum of the two shapes' constraints towards the Chebyshev centre of
+// A n B (weights max(0, 1 - (c_k - min)/tau)^2 -- no transcendental -- with the
+// softness and the step shrinking geometrically), from one of kCertStarts
+// starting points: start 0 is the best of the two centres, their midpoint and
+// the point between the closest points of the two cores where the cores' depth
+// estimates meet; start s > 0 is one of those four moved by half the smaller
+// core radius along an axis of either shape.  The wave runs one start per lane
+// and keeps the deepest (traj_scan_body); deep_common_point runs them in turn.
+constexpr int kCertStarts = 64;
+constexpr int kCertIters = 8;
+
+IKG_HD inline void deep_point_from(const Shape<float>& A, const Shape<float>& B, int start, float* p) {
   float a0[3], a1[3], b0[3], b1[3], ra, rb, s[3], t[3];
   shape_core(A, a0, a1, ra);
   shape_core(B, b0, b1, rb);
@@ -936,22 +939,34 @@ IKG_HD inline void deep_point_search(const Shape<float>& A, const Shape<float>& 
   for (int i = 0; i < 3; ++i) D += (t[i] - s[i]) * (t[i] - s[i]);
   D = sqrtf(D);
   const float fm = D > 0.f ? fminf(fmaxf((D + ra - rb) / (2.f * D), 0.f), 1.f) : 0.5f;
-  float best = -1e30f;
+  float best = -1e30f, base[4][3];
+  int bi = 0;
   for (int cnd = 0; cnd < 4; ++cnd) {
-    float x[3];
     for (int i = 0; i < 3; ++i)
-      x[i] = cnd == 0 ? s[i] + fm * (t[i] - s[i]) : cnd == 1 ? A.t[i] : cnd == 2 ? B.t[i] : 0.5f * (A.t[i] + B.t[i]);
-    const float r = fminf(shape_depth(A, x), shape_depth(B, x));
+      base[cnd][i] = cnd == 0 ? s[i] + fm * (t[i] - s[i]) : cnd == 1 ? A.t[i] : cnd == 2 ? B.t[i]
+                                                                       : 0.5f * (A.t[i] + B.t[i]);
+    const float r = fminf(shape_depth(A, base[cnd]), shape_depth(B, base[cnd]));
     if (r > best) {
       best = r;
-      for (int i = 0; i < 3; ++i) p[i] = x[i];
+      bi = cnd;
     }
+  }
+  float x[3];
+  if (start == 0) {
+    for (int i = 0; i < 3; ++i) x[i] = base[bi][i];
+  } else {
+    const int b = start & 3, j = (start >> 2) % 3, side = (start / 12) & 1, sg = (start / 24) & 1;
+    const float mag = 0.5f * fmaxf(fminf(ra, rb), 1e-3f) * (1.f + (float)(start / 48));
+    const Shape<float>& S = side ? B : A;
+    for (int i = 0; i < 3; ++i) x[i] = base[b][i] + (sg ? -mag : mag) * (S.kind == kSphere ? (i == j ? 1.f : 0.f)
+                                                                                             : S.R[3 * i + j]);
   }
   float scale = 0.f;
   for (int i = 0; i < 3; ++i) scale = fmaxf(scale, fmaxf(A.dims[i], B.dims[i]));
-  float x[3] = {p[0], p[1], p[2]};
   float tau = 0.2f * scale, eta = 0.5f * scale;
-  for (int it = 0; it < IKG_DEEP_ITERS; ++it) {
+  best = -1e30f;
+  for (int i = 0; i < 3; ++i) p[i] = x[i];
+  for (int it = 0; it <= kCertIters; ++it) {
     float ca[6], ga[6][3], cb[6], gb[6][3];
     shape_constraints(A, x, ca, ga);
     shape_constraints(B, x, cb, gb);
@@ -962,6 +977,7 @@ IKG_HD inline void deep_point_search(const Shape<float>& A, const Shape<float>& 
       best = m;
       for (int i = 0; i < 3; ++i) p[i] = x[i];
     }
+    if (it == kCertIters) break;
     const float itau = 1.f / tau;
     float u[3] = {0.f, 0.f, 0.f}, wsum = 0.f;
 #pragma unroll
@@ -980,149 +996,245 @@ IKG_HD inline void deep_point_search(const Shape<float>& A, const Shape<float>& 
   }
 }
 
-// A point deep inside both shapes and the radius of the ball around it that
-// lies in both (<= 0: none found).  The point comes from the fp32 search
-// above; its depth is evaluated exactly in the solve's type, so the search
-// only decides how large the certified radius is, never whether it holds (on
-// random colliding fixture poses it finds a positive radius for ~97% of the
-// colliding pairs; a full optimiser: all of them).
+// fp32 copies of a shape's placement and dimensions (for the search)
 template <typename T>
-IKG_HD inline T deep_common_point(const Shape<T>& A, const Shape<T>& B, T* p) {
-  float RA[9], tA[3], dA[3], RB[9], tB[3], dB[3];
-  for (int i = 0; i < 9; ++i) {
-    RA[i] = (float)A.R[i];
-    RB[i] = (float)B.R[i];
-  }
+IKG_HD inline void shape_f32(const Shape<T>& S, float* R, float* t, float* d) {
+  for (int i = 0; i < 9; ++i) R[i] = (float)S.R[i];
   for (int i = 0; i < 3; ++i) {
-    tA[i] = (float)A.t[i];
-    tB[i] = (float)B.t[i];
-    dA[i] = (float)A.dims[i];
-    dB[i] = (float)B.dims[i];
+    t[i] = (float)S.t[i];
+    d[i] = (float)S.dims[i];
   }
+}
+
+// Start `start`'s point and its exact ball radius in both shapes (in T).
+template <typename T>
+IKG_HD inline T deep_point_depth(const Shape<T>& A, const Shape<T>& B, int start, T* p) {
+  float RA[9], tA[3], dA[3], RB[9], tB[3], dB[3], pf[3];
+  shape_f32(A, RA, tA, dA);
+  shape_f32(B, RB, tB, dB);
   const Shape<float> Af{RA, tA, dA, A.kind}, Bf{RB, tB, dB, B.kind};
-  float pf[3];
-  deep_point_search(Af, Bf, pf);
+  deep_point_from(Af, Bf, start, pf);
   for (int i = 0; i < 3; ++i) p[i] = T(pf[i]);
   return fmin(shape_depth(A, p), shape_depth(B, p));
 }
 
+// A point deep inside both shapes and the radius of the ball around it that
+// lies in both (<= 0: none found): the deepest of the kCertStarts searches
+// (ties: the lowest start), as the wave's reduction picks it.  The depth of
+// every point is evaluated exactly, so the search only decides how large the
+// certified radius is, never whether it holds (on random colliding fixture
+// poses it finds a positive radius for ~97% of the colliding pairs; a full
+// optimiser: all of them).
+template <typename T>
+IKG_HD inline T deep_common_point(const Shape<T>& A, const Shape<T>& B, T* p) {
+  T best = T(-1e30);
+  for (int st = 0; st < kCertStarts; ++st) {
+    T x[3];
+    const T r = deep_point_depth(A, B, st, x);
+    if (r > best) {
+      best = r;
+      for (int i = 0; i < 3; ++i) p[i] = x[i];
+    }
+  }
+  return best;
+}
+
 // Certificate of one pair at one iterate: the joints below the pair's common
 // ancestor with their values at the iterate and lever arms |p - o_k|.
-constexpr int kCertJoints = 2 * kMaxNq;
+constexpr int kCertJoints = kMaxNq;  // the two branches below the common ancestor are disjoint
+constexpr int kCoverBatch = 16;  // ball_covers' one batch of loads (two 6-7-joint chains fit)
 template <typename T>
 struct BallCert {
   T r;  // certified radius, net of rounding; <= 0: no certificate
   int32_t n;
   int32_t joint[kCertJoints];
   int32_t side[kCertJoints];  // which geometry the joint moves
+  int32_t off[kCertJoints];   // the joint's column in q (sl[joint]); entries n .. kCoverBatch - 1: zero
   T qc[kCertJoints];
   T lev[kCertJoints];
-  // ball_cert's working arrays (LDS in the scan: one lane's dynamically
-  // indexed arrays there would live in scratch memory)
-  T org[kCertJoints][3];  // joint origins at the certified iterate
-  T P[2][12];             // the two geometries' placements
-  int32_t up[kMaxNq];     // a joint chain, leaf first
+  // working state (LDS in the scan, where dynamically indexed per-lane arrays
+  // would live in scratch memory): the pair's joint chains, the joint origins
+  // and the two placements (the chains' local transforms go to a workspace of
+  // kMaxNq x 12 the caller passes: the scan's collision scratch)
+  int32_t g[2];                 // the pair's geometries
+  int32_t lca;                  // their joints' lowest common ancestor (-1: none)
+  int32_t nl[3];                // chain lengths: root .. lca, lca .. geometry 0, lca .. geometry 1
+  int32_t list[3][kMaxNq];      // each chain, leaf first (joint indices)
+  T org[kCertJoints][3];        // joint origins at the certified iterate
+  T P[2][12];                   // the two geometries' placements
+  T p[3];                       // the certified point
 };
 
-// Build the certificate for `pair` at configuration q (q[sl[k]] = joint k:
-// a record row and its slot map).  One lane's work.
+// The pair's chains (one lane): geometries, common ancestor, the joints from
+// the root to it and from it to each geometry's joint (`par`: jparent, e.g.
+// staged in LDS).
 template <typename T>
-IKG_HD inline void ball_cert(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c, int pair,
-                             const T* __restrict__ q, const int32_t* sl, const T* tgt, BallCert<T>& out) {
+IKG_HD inline void cert_chains(const KCollision<T>* __restrict__ c, const int32_t* par, int pair, BallCert<T>& out) {
   const int gg[2] = {c->pairs[pair][0], c->pairs[pair][1]};
   int jj[2];
-  for (int h = 0; h < 2; ++h) jj[h] = gg[h] == c->target_geom ? -1 : c->joint[gg[h]];
+  for (int h = 0; h < 2; ++h) {
+    out.g[h] = gg[h];
+    jj[h] = gg[h] == c->target_geom ? -1 : c->joint[gg[h]];
+  }
   int lca = -1;
   if (jj[0] >= 0 && jj[1] >= 0) {
     uint32_t anc = 0;
-    for (int k = jj[0]; k >= 0; k = m->jparent[k]) anc |= 1u << k;
+    for (int k = jj[0]; k >= 0; k = par[k]) anc |= 1u << k;
     lca = jj[1];
-    while (lca >= 0 && !((anc >> lca) & 1u)) lca = m->jparent[lca];
+    while (lca >= 0 && !((anc >> lca) & 1u)) lca = par[lca];
   }
-  // the common ancestor's world frame (root .. lca)
-  T Fs[12] = {T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0)};
-  int32_t* up = out.up;
-  int nu = 0;
-  for (int k = lca; k >= 0 && nu < kMaxNq; k = m->jparent[k]) up[nu++] = k;
+  out.lca = lca;
   int n = 0;
-  for (int pass = 0; pass < 3; ++pass) {
-    // pass 0: root .. lca into Fs; passes 1, 2: each geometry's branch below lca
-    const int h = pass - 1;
-    if (pass > 0) {
-      const int g = gg[h];
-      if (g == c->target_geom || jj[h] < 0) {
+  for (int k = lca; k >= 0 && n < kMaxNq; k = par[k]) out.list[0][n++] = k;
+  out.nl[0] = n;
+  for (int h = 0; h < 2; ++h) {
+    n = 0;
+    if (gg[h] != c->target_geom && jj[h] >= 0)
+      for (int k = jj[h]; k != lca && k >= 0 && n < kMaxNq; k = par[k]) out.list[1 + h][n++] = k;
+    out.nl[1 + h] = n;
+  }
+}
+
+// Local transform of entry e (chains in order) at configuration q.
+template <typename T>
+IKG_HD inline void cert_local(const KModel<T>* __restrict__ m, const T* __restrict__ q, const int32_t* sl, int e,
+                              BallCert<T>& out, T (*Lt)[12]) {
+  const int ch = e < out.nl[0] ? 0 : e < out.nl[0] + out.nl[1] ? 1 : 2;
+  const int i = e - (ch > 0 ? out.nl[0] : 0) - (ch > 1 ? out.nl[1] : 0);
+  const int k = out.list[ch][i];
+  T sk, ck;
+  Prec<T>::sincos_(q[sl[k]], &sk, &ck);
+  joint_local(m, k, sk, ck, Lt[e]);  // entries in chain order: chain 0, then 1, then 2
+}
+
+// Compose the chains (one lane): the common ancestor's frame, then each
+// branch down to its geometry: joint origins, the moving joints' list, the
+// two placements.
+template <typename T>
+IKG_HD inline void cert_compose(const KCollision<T>* __restrict__ c, const T* __restrict__ q, const int32_t* sl,
+                                const T* tgt, BallCert<T>& out, const T (*Lt)[12]) {
+  T Fs[12] = {T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0), T(1), T(0), T(0), T(0)};
+  int n = 0;
+  for (int ch = 0; ch < 3; ++ch) {
+    const int h = ch - 1;
+    if (ch > 0) {
+      const int g = out.g[h];
+      if (g == c->target_geom || c->joint[g] < 0) {
         for (int i = 0; i < 9; ++i) out.P[h][i] = g == c->target_geom ? tgt[i] : c->R[g][i];
         for (int i = 0; i < 3; ++i) out.P[h][9 + i] = g == c->target_geom ? tgt[9 + i] : c->t[g][i];
         continue;
       }
-      nu = 0;
-      for (int k = jj[h]; k != lca && k >= 0 && nu < kMaxNq; k = m->jparent[k]) up[nu++] = k;
     }
     T W[12];
-#pragma unroll
-    for (int i = 0; i < 12; ++i) W[i] = pass == 0 ? ((i == 0 || i == 4 || i == 8) ? T(1) : T(0)) : Fs[i];
-    for (int u = nu - 1; u >= 0; --u) {  // down the chain: W <- W L_k
-      const int k = up[u];
-      T L[12], Rn[9], tn[3], sk, ck;
-      const T qk = q[sl[k]];
-      Prec<T>::sincos_(qk, &sk, &ck);
-      joint_local(m, k, sk, ck, L);
+    for (int i = 0; i < 12; ++i) W[i] = ch == 0 ? ((i == 0 || i == 4 || i == 8) ? T(1) : T(0)) : Fs[i];
+    for (int u = out.nl[ch] - 1; u >= 0; --u) {  // down the chain: W <- W L_k
+      const T* L = Lt[(ch > 0 ? out.nl[0] : 0) + (ch > 1 ? out.nl[1] : 0) + u];
+      T Rn[9], tn[3];
       matmul3(W, L, Rn);
       matvec3(W, L + 9, tn);
-#pragma unroll
       for (int i = 0; i < 9; ++i) W[i] = Rn[i];
-#pragma unroll
       for (int i = 0; i < 3; ++i) W[9 + i] += tn[i];
-      if (pass > 0 && n < kCertJoints) {
+      if (ch > 0 && n < kCertJoints) {
+        const int k = out.list[ch][u];
         out.joint[n] = k;
         out.side[n] = h;
-        out.qc[n] = qk;
-#pragma unroll
+        out.off[n] = sl[k];
+        out.qc[n] = q[sl[k]];
         for (int i = 0; i < 3; ++i) out.org[n][i] = W[9 + i];
         ++n;
       }
     }
-    if (pass == 0) {
-#pragma unroll
+    if (ch == 0) {
       for (int i = 0; i < 12; ++i) Fs[i] = W[i];
     } else {
-      const int g = gg[h];
+      const int g = out.g[h];
       T Rg[9], tg3[3];
       matmul3(W, c->R[g], Rg);
       matvec3(W, c->t[g], tg3);
-#pragma unroll
       for (int i = 0; i < 9; ++i) out.P[h][i] = Rg[i];
-#pragma unroll
       for (int i = 0; i < 3; ++i) out.P[h][9 + i] = W[9 + i] + tg3[i];
     }
   }
-  T PA[12], PB[12];
-#pragma unroll
+  out.n = n;
+  for (int e = n; e < kCoverBatch; ++e) {  // unused batch entries weigh nothing (ball_covers)
+    out.joint[e] = out.side[e] = out.off[e] = 0;
+    out.qc[e] = T(0);
+  }
+}
+
+// The two geometries as shapes (their placements copied out of `out`).
+template <typename T>
+IKG_HD inline void cert_shapes(const KCollision<T>* __restrict__ c, const BallCert<T>& out, T (&PA)[12], T (&PB)[12],
+                               Shape<T>& A, Shape<T>& B) {
   for (int i = 0; i < 12; ++i) {
     PA[i] = out.P[0][i];
     PB[i] = out.P[1][i];
   }
-  const Shape<T> A{PA, PA + 9, c->dims[gg[0]], c->kind[gg[0]]};
-  const Shape<T> B{PB, PB + 9, c->dims[gg[1]], c->kind[gg[1]]};
-  T p[3];
-  const T r = deep_common_point(A, B, p);
-  out.n = n;
-  for (int e = 0; e < n; ++e) {
+  A = Shape<T>{PA, PA + 9, c->dims[out.g[0]], c->kind[out.g[0]]};
+  B = Shape<T>{PB, PB + 9, c->dims[out.g[1]], c->kind[out.g[1]]};
+}
+
+// The radius (net of the placements' rounding: 1e-9 fp64, 1e-5 fp32, as the
+// EPA certificate) and the lever arms |p - o_k| for the point found.
+template <typename T>
+IKG_HD inline void cert_finish(T r, const T* p, BallCert<T>& out) {
+  for (int i = 0; i < 3; ++i) out.p[i] = p[i];
+  for (int e = 0; e < out.n; ++e) {
     const T d[3] = {p[0] - out.org[e][0], p[1] - out.org[e][1], p[2] - out.org[e][2]};
     out.lev[e] = sqrt(dot3(d, d));
   }
   out.r = r - (sizeof(T) == 8 ? T(1e-9) : T(1e-5));
 }
 
-// Does the certificate prove the pair intersecting at configuration q?
+// Build the certificate for `pair` at configuration q (q[sl[k]] = joint k:
+// a record row and its slot map), one lane doing every stage in turn (the host
+// emulator; the scan runs the same stages over the wave, traj_scan_body).
 template <typename T>
-IKG_HD inline bool ball_covers(const BallCert<T>& bc, const T* __restrict__ q, const int32_t* sl) {
+IKG_HD inline void ball_cert(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c, int pair,
+                             const T* __restrict__ q, const int32_t* sl, const T* tgt, BallCert<T>& out) {
+  cert_chains(c, m->jparent, pair, out);
+  T Lt[kMaxNq][12];
+  for (int e = 0; e < out.nl[0] + out.nl[1] + out.nl[2]; ++e) cert_local(m, q, sl, e, out, Lt);
+  cert_compose(c, q, sl, tgt, out, Lt);
+  T PA[12], PB[12];
+  Shape<T> A{}, B{};
+  cert_shapes(c, out, PA, PB, A, B);
+  T p[3];
+  const T r = deep_common_point(A, B, p);
+  cert_finish(r, p, out);
+}
+
+// Does the certificate prove the pair intersecting at configuration q (q[off]:
+// a record row, or a configuration in joint order with the slot map the
+// certificate was built with)?  Up to kCoverBatch joints the loads go out as
+// one batch (unused entries read q[0] and weigh nothing) instead of one
+// dependent global load per joint (the scan's cover step ran ~35k cycles per
+// chunk that way, profiles/r05/collision/).
+template <typename T>
+IKG_HD inline bool ball_covers(const BallCert<T>& bc, const T* __restrict__ q) {
   T s0[2] = {T(0), T(0)}, s1[2] = {T(0), T(0)};
-  for (int e = 0; e < bc.n; ++e) {
-    const T d = fabs(q[sl[bc.joint[e]]] - bc.qc[e]);
-    const int h = bc.side[e];
-    s0[h] += d;
-    s1[h] += d * bc.lev[e];
+  const int n = bc.n;
+  if (n <= kCoverBatch) {
+    T v[kCoverBatch];
+#pragma unroll
+    for (int e = 0; e < kCoverBatch; ++e) v[e] = q[bc.off[e]];
+#pragma unroll
+    for (int e = 0; e < kCoverBatch; ++e) {
+      const T d = e < n ? fabs(v[e] - bc.qc[e]) : T(0);
+      const T l = bc.lev[e < n ? e : 0];
+      const bool h1 = bc.side[e] != 0;
+      s0[0] += h1 ? T(0) : d;
+      s0[1] += h1 ? d : T(0);
+      s1[0] += h1 ? T(0) : d * l;
+      s1[1] += h1 ? d * l : T(0);
+    }
+  } else {
+    for (int e = 0; e < n; ++e) {
+      const T d = fabs(q[bc.off[e]] - bc.qc[e]);
+      const int h = bc.side[e];
+      s0[h] += d;
+      s1[h] += d * bc.lev[e];
+    }
   }
   return bc.r > T(0) && s1[0] + bc.r * s0[0] < bc.r && s1[1] + bc.r * s0[1] < bc.r;
 }

@@ -281,7 +281,7 @@ void emu_ball(const ikg_model_desc* d, const ikg_collision_desc* cd, int pair, c
   static thread_local ikg::BallCert<T> bc;
   ikg::ball_cert(&m, &kc, pair, (const T*)qc, sl, (const T*)target, bc);
   *r_out = (double)bc.r;
-  for (int64_t i = 0; i < B; ++i) covered[i] = ikg::ball_covers(bc, (const T*)q + d->nq * i, sl) ? 1 : 0;
+  for (int64_t i = 0; i < B; ++i) covered[i] = ikg::ball_covers(bc, (const T*)q + d->nq * i) ? 1 : 0;
 }
 
 extern "C" int ikg_emu_ball_cert(const ikg_model_desc* d, const ikg_collision_desc* cd, int dtype, int pair,

@@ -45,7 +45,7 @@ namespace ikg {
 template <typename T, bool DAMPED, class SP>
 constexpr int kPairMinWaves = (kFrame1<SP> && !DAMPED) ? (sizeof(T) == 8 ? 2 : 4) : 1;
 
-template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
+template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false, bool POOL = false>
 __global__ __launch_bounds__(64)
 #if IKG_WPE
 __attribute__((amdgpu_waves_per_eu(1, IKG_WPE)))
@@ -63,7 +63,7 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
   // model tables stay in global memory: the compiler hoists them into
   // registers (staging them in LDS and re-reading per iteration measured 8%
   // slower)
-  pair_batch_body<T, DAMPED, SP, MED, REC>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
+  pair_batch_body<T, DAMPED, SP, MED, REC, POOL>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
                                            err_out, rec, rec_n, pool);
 }
 
@@ -209,6 +209,14 @@ static size_t lds_pad_bytes() {
   return (size_t)v;
 }
 
+static int64_t packed_min_batch();
+
+// IKG_PAIR_ILP=0: the default-scheduled pair kernel for every launch (A/B knob)
+static bool pair_ilp_on() {
+  static const bool v = !(getenv("IKG_PAIR_ILP") && atoi(getenv("IKG_PAIR_ILP")) == 0);
+  return v;
+}
+
 template <typename T, bool DAMPED, class SP>
 static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, hipStream_t s) {
   const int ppw = a.ppw;
@@ -223,15 +231,26 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
   // fp32 answer does not depend on how q0 was passed
   if constexpr (kFrame1<SP> && !DAMPED) {
     const bool med = a.S > 1 || a.q0_stride != 0 || force_med || std::is_same<T, float>::value;
-    if (a.rec) {  // collision continuation records (ikg_collision.hip)
+    // fp32, no records, at most one wave per SIMD: the max-ILP build of the
+    // same kernel (ikg_pair_ilp.hip)
+    if constexpr (std::is_same<SP, SpecNextage>::value && std::is_same<T, float>::value)
+      if (!a.rec && pair_ilp_on() && (int64_t)grid.x * 32 < packed_min_batch()) {
+        (void)launch_pair_ilp(dmodel, prm, a, med, lds_pad_bytes(), s);
+        return;
+      }
+    if (a.rec) {  // collision continuation records (ikg_collision.hip): fixed slots or the pool
+      auto go = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(64), lds_pad_bytes(), s, dmodel, prm, (const T*)a.targets,
+                           (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out, a.converged, a.iters,
+                           (T*)a.err_out, (T*)a.rec, a.rec_n, a.rec_pool);
+      };
+      const bool pool = a.rec_pool.cursor != nullptr;
       if (med)
-        hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, true, true>), grid, dim3(64), lds_pad_bytes(), s,
-                           dmodel, prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw,
-                           (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n, a.rec_pool);
+        pool ? go(ikg_pair_batch_kernel<T, DAMPED, SP, true, true, true>)
+             : go(ikg_pair_batch_kernel<T, DAMPED, SP, true, true, false>);
       else
-        hipLaunchKernelGGL((ikg_pair_batch_kernel<T, DAMPED, SP, false, true>), grid, dim3(64), lds_pad_bytes(), s,
-                           dmodel, prm, (const T*)a.targets, (const T*)a.q0, a.q0_stride, a.B, a.S, ppw,
-                           (T*)a.q_out, a.converged, a.iters, (T*)a.err_out, (T*)a.rec, a.rec_n, a.rec_pool);
+        pool ? go(ikg_pair_batch_kernel<T, DAMPED, SP, false, true, true>)
+             : go(ikg_pair_batch_kernel<T, DAMPED, SP, false, true, false>);
       if (a.rec_used) *a.rec_used = true;
       return;
     }

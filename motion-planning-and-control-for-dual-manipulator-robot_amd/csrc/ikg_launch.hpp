@@ -343,6 +343,11 @@ template <typename T>
 hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,
                              hipStream_t s);
 
+// pair layout, Nextage specialisation, lambda = 0, built with the max-ILP
+// scheduler for launches of at most one wave per SIMD (ikg_pair_ilp.hip)
+hipError_t launch_pair_ilp(const KModel<float>* dmodel, const KParams<float>& prm, const BatchArgs& a, bool med,
+                           size_t lds, hipStream_t s);
+
 // packed fp32 layout, Nextage specialisation (ikg_packed.hip)
 hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>& prm, const BatchArgs& a,
                                hipStream_t s);

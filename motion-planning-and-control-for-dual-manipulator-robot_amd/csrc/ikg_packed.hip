@@ -7,6 +7,7 @@
 
 #include <atomic>
 #include <cstdlib>
+#include <type_traits>
 
 #include "ikg_device.hpp"
 #include "ikg_launch.hpp"
@@ -33,7 +34,7 @@ namespace ikg {
 // REC: the collision continuation's records (ikg_collision.hip §3b), written
 // from the first passing iterate on, both arms' blocks by the problem's lane;
 // the outputs at that iterate come from its record 0 (solve_pair).
-template <class SP, int WPS, bool MED, bool REC = false>
+template <class SP, int WPS, bool MED, bool REC = false, bool POOL = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPS == 0 ? 3 : WPS)))
 void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               KParams<float> prm, const float* __restrict__ targets,
@@ -63,15 +64,15 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
   v2f nrm, other;
   if constexpr (REC) {
     const int rl = rec_len(m->n_passive);
-    RecOut<float> ro{pool.cursor ? rec : rec + p * (int64_t)(prm.max_iters + 1) * rl, rec_n + p, qrow,
+    RecOut<float> ro{POOL ? rec : rec + p * (int64_t)(prm.max_iters + 1) * rl, rec_n + p, qrow,
                      q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl};
-    if (pool.cursor) {
+    if constexpr (POOL) {
       ro.pool = pool;
       ro.pool.base = pool.base + p;
       pool.base[p] = -1;
     }
     rec_n[p] = 0;
-    if (solve_pair<v2f, false, SP, MED, true>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
+    if (solve_pair<v2f, false, SP, MED, true, POOL>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
     solve_pair<v2f, false, SP, MED>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
   }
@@ -123,7 +124,7 @@ static unsigned simd_count() {
 
 // The cap instantiation really fits WPS waves per SIMD (4 WPS single-wave
 // workgroups per CU) on this device; otherwise the uncapped kernel runs.
-template <int WPS, bool REC = false>
+template <int WPS, bool REC = false, bool POOL = false>
 static bool capped_ok() {
   constexpr int kDevs = 64;
   static std::atomic<int> cache[kDevs];  // 0 unknown, 1 ok, 2 not
@@ -133,7 +134,7 @@ static bool capped_ok() {
   if (!v) {
     int blocks = 0;
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, true, REC>), 64, packed_lds_pad());
+        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, true, REC, POOL>), 64, packed_lds_pad());
     v = (e == hipSuccess && blocks == 4 * WPS) ? 1 : 2;
     cache[dev].store(v, std::memory_order_relaxed);
   }
@@ -154,12 +155,19 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
 #define IKG_PACKED_REC 1
 #endif
   if (IKG_PACKED_REC && a.rec) {  // collision continuation records (0: A/B knob, the trajectory kernel instead)
-    if (need == 1 && capped_ok<1, true>())
-      go(ikg_packed_batch_kernel<SpecNextage, 1, true, true>);
-    else if (need == 2 && capped_ok<2, true>())
-      go(ikg_packed_batch_kernel<SpecNextage, 2, true, true>);
+    auto rec = [&](auto pool) {  // fixed slots or the pool (solve_pair POOL)
+      constexpr bool P = decltype(pool)::value;
+      if (need == 1 && capped_ok<1, true, P>())
+        go(ikg_packed_batch_kernel<SpecNextage, 1, true, true, P>);
+      else if (need == 2 && capped_ok<2, true, P>())
+        go(ikg_packed_batch_kernel<SpecNextage, 2, true, true, P>);
+      else
+        go(ikg_packed_batch_kernel<SpecNextage, 0, true, true, P>);
+    };
+    if (a.rec_pool.cursor)
+      rec(std::true_type{});
     else
-      go(ikg_packed_batch_kernel<SpecNextage, 0, true, true>);
+      rec(std::false_type{});
     if (a.rec_used) *a.rec_used = true;
     return hipGetLastError();
   }

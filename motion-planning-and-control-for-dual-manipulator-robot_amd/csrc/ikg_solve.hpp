@@ -115,7 +115,10 @@ __device__ inline bool both_below(T x, T xo, E eps2) {
 // float: this lane owns one arm (pair layout, partner = lane ^ 1); T = v2f:
 // this lane owns both arms (packed layout).  Returns (through refs) the final
 // q of this lane, the update count and the hand error norms at the returned q.
-template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
+// POOL (with REC): records reserved from the pool at the first passing
+// iterate; without it, this problem's fixed slot (no reservation state in the
+// loop: with it, the fixed-slot kernel ran 12% slower at C2, profiles/r05/collision/)
+template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false, bool POOL = false>
 __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
                                   const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
                                   T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out,
@@ -190,7 +193,7 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
       if (pass && k0 < 0) {  // the answer unless it collides: record 0, written out after the loop
         k0 = it;
         conv = true;
-        if (ro->pool.cursor) {  // reserve this problem's records in the pool
+        if constexpr (POOL) {  // reserve this problem's records in the pool
           const unsigned long long need = (unsigned long long)(prm.max_iters + 1 - it);
           unsigned long long b = 0;
           if constexpr (is_packed<T>) {
@@ -206,7 +209,8 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
           if (arm == 0) *ro->pool.base = norec ? -1 : (int32_t)b;
         }
       }
-      if (norec) break;  // no room: end at k0 as the loop without records would
+      if constexpr (POOL)
+        if (norec) break;  // no room: end at k0 as the loop without records would
       if (k0 >= 0) {
         if constexpr (is_packed<T>) {  // both arms' blocks from the one lane
           float b0[8], b1[8];
@@ -304,7 +308,7 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 // model-specialised kernels ikg_jit.cpp compiles at run time with `m` pointing
 // at a constant copy of the model tables): one 64-lane wave per workgroup
 // holding `ppw` problems on lanes [0, 2 ppw).
-template <typename T, bool DAMPED, class SP, bool MED, bool REC = false>
+template <typename T, bool DAMPED, class SP, bool MED, bool REC = false, bool POOL = false>
 __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KParams<T>& prm,
                                        const T* __restrict__ targets, const T* __restrict__ q0, int64_t q0_stride,
                                        int64_t B, int64_t S, int ppw, T* __restrict__ q_out,
@@ -328,15 +332,15 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
   T nrm, other;
   if constexpr (REC) {  // the continuation's records (ikg_collision.hip): outputs at the first passing iterate
     const int rl = rec_len(m->n_passive);
-    RecOut<T> ro{pool.cursor ? rec : rec + p * (int64_t)(prm.max_iters + 1) * rl, nrec + p, qrow, q_out + p * m->nq,
+    RecOut<T> ro{POOL ? rec : rec + p * (int64_t)(prm.max_iters + 1) * rl, nrec + p, qrow, q_out + p * m->nq,
                  conv_out + p, iters_out + p, err_out + p * 2, rl};
-    if (pool.cursor) {
+    if constexpr (POOL) {
       ro.pool = pool;
       ro.pool.base = pool.base + p;
       if (arm == 0) pool.base[p] = -1;
     }
     if (arm == 0) nrec[p] = 0;
-    if (solve_pair<T, DAMPED, SP, MED, true>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
+    if (solve_pair<T, DAMPED, SP, MED, true, POOL>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
     solve_pair<T, DAMPED, SP, MED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
   }

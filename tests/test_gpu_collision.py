@@ -420,3 +420,22 @@ def test_pooled_records_c3_fp32(csolver, monkeypatch):
     print(f"C3 fp32 pooled records vs trajectory kernel: {int((~same).sum())} of 65536 differ in flag or count")
     assert same.mean() >= 0.999
     assert np.abs(a.q[same] - b.q[same]).max() <= 1e-3
+
+
+@pytest.mark.parametrize("dtype", ["f64", "f32"])
+def test_scan_certificates_do_not_change_answers(csolver, dtype, monkeypatch):
+    """The records scan's inscribed-ball certificates (ikg_collision.hip
+    scan_ball_cert / ball_covers) only skip narrow phases whose answer is
+    "colliding": C2's 4,096 targets with the collision term give the same bits
+    with them (IKG_SCAN_CERT=1) and without (0), and they do prove records
+    here (the fixture's colliding passes)."""
+    from ikgrasp.workload import uniform_targets
+    tg = uniform_targets(4096, seed=0)
+    out = {}
+    for c in ("1", "0"):
+        monkeypatch.setenv("IKG_SCAN_CERT", c)
+        out[c] = csolver.solve(tg, np.zeros(15), dtype=dtype, check_collision=True)
+    a, b = out["1"], out["0"]
+    for x, y in zip((a.q, a.converged, a.iters, a.err), (b.q, b.converged, b.iters, b.err)):
+        assert np.array_equal(x, y)
+    assert 0 < int(a.converged.sum()) < 4096

@@ -1,6 +1,8 @@
 """Trajectory-scan statistics (diagnostic build -DIKG_CPROF: `bash tools/cprof.sh`):
 per problem and window, the full checks, sweeps, lane-parallel witness rounds
-and shader cycles of traj_scan (max and mean)."""
+and shader cycles of traj_scan (max and mean), and the inscribed-ball
+certificates' counts (built, positive; records tested against one and proved
+by one)."""
 import ctypes as C
 import json
 import os
@@ -26,7 +28,7 @@ lib = _lib.load()
 lib.ikg_debug_scan.argtypes = [C.c_void_p, C.c_int]
 tdt = torch.float64 if dtype == "f64" else torch.float32
 tg = torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device="cuda")
-buf = np.zeros(8, np.uint64)
+buf = np.zeros(24, np.uint64)
 s.solve(tg, torch.zeros(15, dtype=tdt), check_collision=True)
 torch.cuda.synchronize()
 lib.ikg_debug_scan(buf.ctypes.data, 1)
@@ -36,4 +38,10 @@ lib.ikg_debug_scan(buf.ctypes.data, 1)
 n = max(int(buf[5]), 1)
 print(json.dumps({"batch": B, "dtype": dtype, "problem_windows": n, "checks_max": int(buf[0]),
                   "checks_mean": int(buf[1]) / n, "cycles_max": int(buf[2]), "cycles_mean": int(buf[7]) / n,
-                  "sweeps_sum": int(buf[3]), "lane_rounds_max": int(buf[4]), "lane_rounds_sum": int(buf[6])}))
+                  "sweeps_sum": int(buf[3]), "lane_rounds_max": int(buf[4]), "lane_rounds_sum": int(buf[6]),
+                  "certificates": int(buf[8]), "certificates_positive": int(buf[9]),
+                  "records_tested_against_a_certificate": int(buf[10]), "records_proved_by_a_certificate": int(buf[11]),
+                  "cert_cycles_placements": int(buf[12]), "cert_cycles_search": int(buf[13]),
+                  "cert_cycles_finish": int(buf[14]), "witness_and_check_cycles": int(buf[15]),
+                  "chunk_cert_stage_cycles": int(buf[16]), "passive_fill_cycles": int(buf[17]),
+                  "cover_cycles": int(buf[18]), "cover_calls": int(buf[19])}))
