@@ -759,7 +759,7 @@ __device__ __forceinline__ void cont_update(const KModel<T>* __restrict__ m, con
 #pragma unroll
   for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
   arm_update(m, arm, prm.dt, s, dq, qc, qa);
-  trig_advance(qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);
+  trig_advance<T, IKG_GENERIC_MED>(qc, qa, q_old, ((it + 1) % Trig<T>::kResync) == 0, sn, cs);  // as solve_pair
 }
 
 // Certified-stretch updates (no collision check ahead, so no joint frames):

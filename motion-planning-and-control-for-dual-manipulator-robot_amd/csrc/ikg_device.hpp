@@ -878,6 +878,15 @@ struct Trig;
 #ifndef IKG_RESYNC64
 #define IKG_RESYNC64 128
 #endif
+// the chest-frame path's trig rule (generic models, the damped solve, the
+// collision continuation's chest-frame loop): 2 = the longer series for every
+// step up to kIncMed (the tilted robot's trajectories take steps beyond the
+// short series' range on ~70% of updates, and a divergent exact / series split
+// cost 1.8-2.0 ms against 1.74 at B = 4,096, profiles/r05/generic/); 1 = the
+// frame-1 path's medium-range rule; 0 = the short series or the exact sincos
+#ifndef IKG_GENERIC_MED
+#define IKG_GENERIC_MED 2
+#endif
 template <>
 struct Trig<double> {
   // |d| <= 0.025: the dropped terms d^9/9! and d^8/8! are < 1e-18 relative.
@@ -1281,14 +1290,42 @@ IKG_HD inline void trig_exact(T qc, const T* qa, T* sn, T* cs) {
 }
 
 // advance (sin, cos) after the update q_old -> (qc, qa); exact when `resync`
-// or when any step exceeds the incremental range
-template <typename T>
+// or when any step exceeds the incremental range.  MED: the medium-range rule
+// of the frame-1 path (trig_med_f1) -- the longer series for steps up to
+// kIncMed, exact beyond and at resyncs.
+template <typename T, int MED = 0>
 IKG_HD inline void trig_advance(T qc, const T* qa, const T* q_old, bool resync, T* sn, T* cs) {
   T d[7];
   d[0] = qc - q_old[0];
   bool big = resync;
 #pragma unroll
   for (int k = 0; k < kArmDof; ++k) d[k + 1] = qa[k] - q_old[k + 1];
+  if constexpr (MED == 2) {  // the longer series for every step up to kIncMed: no divergent short/long split
+    T dmax = fabs(d[0]);
+#pragma unroll
+    for (int j = 1; j < 7; ++j) dmax = fmax(dmax, fabs(d[j]));
+#pragma unroll
+    for (int j = 0; j < 7; ++j) Trig<T>::step_med(d[j], sn[j], cs[j]);
+    if (resync || any_of(dmax > T(Trig<T>::kIncMed))) trig_exact(qc, qa, sn, cs);
+    return;
+  }
+  if constexpr (MED == 1) {
+    T dmax = fabs(d[0]);
+#pragma unroll
+    for (int j = 1; j < 7; ++j) dmax = fmax(dmax, fabs(d[j]));
+    if (resync || any_of(dmax > T(Trig<T>::kIncMax))) {
+      if (!resync && all_of(mnot(dmax > T(Trig<T>::kIncMed)))) {
+#pragma unroll
+        for (int j = 0; j < 7; ++j) Trig<T>::step_med(d[j], sn[j], cs[j]);
+      } else {
+        trig_exact(qc, qa, sn, cs);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 7; ++j) Trig<T>::step(d[j], sn[j], cs[j]);
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 7; ++j) big |= any_of(fabs(d[j]) > T(Trig<T>::kIncMax));
   if constexpr (IKG_ABL & 1) {  // timing ablation: no incremental trig

@@ -16,6 +16,7 @@ namespace {
 
 // updates that took the LQ form (pinv_step_*), since the last ikg_emu_lq_count(1)
 thread_local long long lq_count = 0;
+thread_local long long big_count = 0;  // lane-updates whose step leaves the short trig series (chest-frame path)
 thread_local long long jacobi_count = 0;  // arm solves of the LQ form that fell back to the Jacobi sweeps
 thread_local long long svd_count = 0;  // of those, with an arm that pins the chest (bb = 0: rank-deficient M_a)
 // updates whose two arm lanes computed different chest steps (must stay 0:
@@ -162,8 +163,13 @@ void emu_one(const ikg::KModel<T>& m, const ikg::KParams<T>& prm, bool damped, c
       if (f1)
         (med ? trig_advance_f1<T, true> : trig_advance_f1<T, false>)(&m, arm, qc[arm], qa[arm], q_old[arm],
                                                                      (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
-      else
-        trig_advance(qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
+      else {
+        bool big = false;  // the exact sincos outside resyncs (diagnostic count)
+        big |= fabs(qc[arm] - q_old[arm][0]) > T(Trig<T>::kIncMax);
+        for (int k = 0; k < kArmDof; ++k) big |= fabs(qa[arm][k] - q_old[arm][k + 1]) > T(Trig<T>::kIncMax);
+        if (big) ++big_count;
+        trig_advance<T, IKG_GENERIC_MED>(qc[arm], qa[arm], q_old[arm], (it % Trig<T>::kResync) == 0, sn[arm], cs[arm]);
+      }
     }
   }
   for (int j = 0; j < m.nq; ++j) qo[j] = qrow[j];
@@ -214,6 +220,11 @@ void emu(const ikg_model_desc* d, const void* targets, const void* q0, int64_t s
 
 }  // namespace
 
+extern "C" long long ikg_emu_big_count(int reset) {
+  const long long v = big_count;
+  if (reset) big_count = 0;
+  return v;
+}
 extern "C" long long ikg_emu_lq_count(int reset) {
   const long long v = lq_count;
   if (reset) lq_count = 0;

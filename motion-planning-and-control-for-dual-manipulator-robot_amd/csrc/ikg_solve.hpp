@@ -252,7 +252,7 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     if constexpr (F1)
       trig_advance_f1<T, MED>(m, arm, qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
     else
-      trig_advance(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
+      trig_advance<T, MED ? 1 : IKG_GENERIC_MED>(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }
 #ifdef IKG_PAD_OPS
   T ps = T(0);

@@ -71,7 +71,9 @@ def classify(op, line):
 
 def parse(path, kname):
     L = open(path).read().split("\n")
-    start = next(i for i, l in enumerate(L) if re.match(r"^_Z\S*:", l) and kname in l.split(":")[0])
+    labels = [(i, l.split(":")[0]) for i, l in enumerate(L) if re.match(r"^[A-Za-z_]\S*:", l)]
+    exact = [i for i, n in labels if n == kname]  # extern "C" kernels (the hipRTC-specialised ones)
+    start = exact[0] if exact else next(i for i, n in labels if n.startswith("_Z") and kname in n)
     end = next(i for i in range(start, len(L)) if L[i].startswith(".Lfunc_end"))
     blocks, order, cur = {}, [], "entry"
     loc = "?"
