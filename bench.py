@@ -325,12 +325,21 @@ class QGather:
     Host collectives (the gloo rehearsal): synchronous gathers of host copies."""
 
     def __init__(self, dist, q_out, gathered, world, enabled=True, host=False):
-        self.dist, self.gathered, self.host = dist, gathered, host
+        self.dist, self.host = dist, host
         self.on = world > 1 and enabled
         self.overlap = self.on and not host
         self.bufs = [q_out, q_out.new_empty(q_out.shape)] if self.overlap else [q_out]
+        # rank 0's outputs are double-buffered with the inputs: two gathers in
+        # flight never write the same tensors, whatever order the backend
+        # completes them in (gloo runs async work on several threads)
+        self.outs = [gathered] + ([[t.new_empty(t.shape) for t in gathered]] if self.overlap and gathered else
+                                  [gathered] * (len(self.bufs) - 1))
         self.pending = [None] * len(self.bufs)
         self.k = 0
+
+    def result(self):
+        """rank 0: the last submitted step's gathered q (after drain())."""
+        return self.outs[(self.k - 1) % len(self.bufs)]
 
     def buffer(self):
         i = self.k % len(self.bufs)
@@ -346,9 +355,9 @@ class QGather:
         if not self.on:
             return
         if self.overlap:
-            self.pending[i] = self.dist.gather(qb, self.gathered, dst=0, async_op=True)
+            self.pending[i] = self.dist.gather(qb, self.outs[i], dst=0, async_op=True)
         else:
-            self.dist.gather(qb.cpu() if qb.device.type != "cpu" else qb, self.gathered, dst=0)
+            self.dist.gather(qb.cpu() if qb.device.type != "cpu" else qb, self.outs[i], dst=0)
 
     def drain(self):
         for i, w in enumerate(self.pending):

@@ -85,7 +85,8 @@ def _qgather_worker(rank, world, port, host, q):
         ok &= all(w is None for w in g.pending)
         alternates = len(set(ids)) == (1 if host else 2) and all(ids[i] == ids[i % len(g.bufs)] for i in range(5))
         if rank == 0:
-            ok &= all(torch.all(gathered[r] == 40.0 + r).item() for r in range(world))
+            out = g.result()
+            ok &= all(torch.all(out[r] == 40.0 + r).item() for r in range(world))
         q.put((rank, ok and alternates))
     finally:
         dist.destroy_process_group()
