@@ -60,6 +60,7 @@ def lib():
         L = C.CDLL(LIB)
         L.ikg_model_create.argtypes = [C.POINTER(Desc), C.POINTER(_vp)]
         L.ikg_model_destroy.argtypes = [_vp]
+        L.ikg_model_trim.argtypes = [_vp]  # hand pooled scratch back to the runtime (include/ikgrasp.h)
         L.ikg_solve_batch.argtypes = [_vp, C.c_int, C.c_int, _vp, _vp, C.c_int64, C.c_int64, C.POINTER(Params),
                                       _vp, _vp, _vp, _vp, _vp, C.c_uint32]
         L.ikg_model_set_collision.argtypes = [_vp, C.POINTER(CDesc)]
