@@ -58,6 +58,9 @@ IKG_HD inline int rec_len(int n_passive) { return kRecPassive + ((n_passive + 3)
 
 template <typename T>
 __device__ __forceinline__ void store_block8(T* dst, const T (&v)[8]) {
+#if defined(IKG_REC_NOSTORE)  // timing ablation only: records not written (answers wrong)
+  (void)dst, (void)v;
+#else
   struct alignas(16) V16 {
     T x[16 / sizeof(T)];
   };
@@ -69,6 +72,7 @@ __device__ __forceinline__ void store_block8(T* dst, const T (&v)[8]) {
     for (int e = 0; e < per; ++e) b.x[e] = v[k * per + e];
     reinterpret_cast<V16*>(dst)[k] = b;
   }
+#endif
 }
 
 template <typename T>
