@@ -1568,6 +1568,15 @@ __device__ inline void scan_ball_cert(const KModel<T>* __restrict__ m, const KCo
 #endif
   if (lane == 0) cert_chains(c, par, pair, bc);
   __syncthreads();
+  if (!bc.ok) {  // wave-uniform (LDS): no certificate
+    __syncthreads();
+    if (lane == 0) {
+      bc.n = 0;
+      bc.r = T(-1);
+    }
+    __syncthreads();
+    return;
+  }
   const int ne = bc.nl[0] + bc.nl[1] + bc.nl[2];
   for (int e = lane; e < ne; e += 64) cert_local(m, q, sl, e, bc, Lt);
   __syncthreads();

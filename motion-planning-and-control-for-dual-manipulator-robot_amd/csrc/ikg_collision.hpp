@@ -1059,6 +1059,7 @@ struct BallCert {
   int32_t g[2];                 // the pair's geometries
   int32_t lca;                  // their joints' lowest common ancestor (-1: none)
   int32_t nl[3];                // chain lengths: root .. lca, lca .. geometry 0, lca .. geometry 1
+  int32_t ok;                   // the chains fit the workspace (a tree of at most kMaxNq joints)
   int32_t list[3][kMaxNq];      // each chain, leaf first (joint indices)
   T org[kCertJoints][3];        // joint origins at the certified iterate
   T P[2][12];                   // the two geometries' placements
@@ -1076,23 +1077,32 @@ IKG_HD inline void cert_chains(const KCollision<T>* __restrict__ c, const int32_
     out.g[h] = gg[h];
     jj[h] = gg[h] == c->target_geom ? -1 : c->joint[gg[h]];
   }
+  // every walk is bounded by kMaxNq steps whatever the tables hold; a chain
+  // that does not end within it leaves the certificate empty (ok = 0)
   int lca = -1;
+  bool ok = true;
   if (jj[0] >= 0 && jj[1] >= 0) {
     uint32_t anc = 0;
-    for (int k = jj[0]; k >= 0; k = par[k]) anc |= 1u << k;
+    int k = jj[0], steps = 0;
+    for (; k >= 0 && k < kMaxNq && steps < kMaxNq; k = par[k], ++steps) anc |= 1u << k;
+    ok = ok && k < 0;
     lca = jj[1];
-    while (lca >= 0 && !((anc >> lca) & 1u)) lca = par[lca];
+    for (steps = 0; lca >= 0 && lca < kMaxNq && steps < kMaxNq && !((anc >> lca) & 1u); ++steps) lca = par[lca];
+    ok = ok && lca < kMaxNq && steps < kMaxNq;
   }
   out.lca = lca;
-  int n = 0;
-  for (int k = lca; k >= 0 && n < kMaxNq; k = par[k]) out.list[0][n++] = k;
+  int n = 0, k = lca;
+  for (; k >= 0 && k < kMaxNq && n < kMaxNq; k = par[k]) out.list[0][n++] = k;
+  ok = ok && k < 0;
   out.nl[0] = n;
   for (int h = 0; h < 2; ++h) {
     n = 0;
-    if (gg[h] != c->target_geom && jj[h] >= 0)
-      for (int k = jj[h]; k != lca && k >= 0 && n < kMaxNq; k = par[k]) out.list[1 + h][n++] = k;
+    k = (gg[h] != c->target_geom && jj[h] >= 0) ? jj[h] : lca;
+    for (; k != lca && k >= 0 && k < kMaxNq && n < kMaxNq; k = par[k]) out.list[1 + h][n++] = k;
+    ok = ok && (k == lca || k < 0);
     out.nl[1 + h] = n;
   }
+  out.ok = ok && out.nl[0] + out.nl[1] + out.nl[2] <= kMaxNq;
 }
 
 // Local transform of entry e (chains in order) at configuration q.
@@ -1193,6 +1203,11 @@ template <typename T>
 IKG_HD inline void ball_cert(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c, int pair,
                              const T* __restrict__ q, const int32_t* sl, const T* tgt, BallCert<T>& out) {
   cert_chains(c, m->jparent, pair, out);
+  if (!out.ok) {
+    out.n = 0;
+    out.r = T(-1);
+    return;
+  }
   T Lt[kMaxNq][12];
   for (int e = 0; e < out.nl[0] + out.nl[1] + out.nl[2]; ++e) cert_local(m, q, sl, e, out, Lt);
   cert_compose(c, q, sl, tgt, out, Lt);
