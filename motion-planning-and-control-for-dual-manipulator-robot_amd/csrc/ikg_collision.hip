@@ -32,7 +32,7 @@ __device__ unsigned long long g_cprof[8];
 __device__ unsigned long long g_skip[8];
 // trajectory scan, per problem and window: max / sum of checks, max cycles,
 // sum / max of sweeps, windows scanned, certificates, sum of cycles
-__device__ unsigned long long g_scan[24];
+__device__ unsigned long long g_scan[28];
 #define SKIP_STAT(i, v) atomicAdd(&g_skip[i], (unsigned long long)(v))
 // single-lane witness work: cycles in GJK (pair_collides + supports), in
 // certify_witness (of which EPA), calls of each
@@ -151,6 +151,12 @@ __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T
     ncand += __popcll(bal);
   }
   __syncthreads();
+#ifdef IKG_CPROF
+  {  // prof[4]: the bounding-sphere pass (its share of the sweep, prof[2])
+    const unsigned long long _n = clock64();
+    if (prof && cp_lead) prof[4] += _n - t;
+  }
+#endif
   for (int base = 0; base < ncand; base += 64) {
     const int i = base + lane;
     const int k = i < ncand ? S.cand[i] : 0;
@@ -952,7 +958,7 @@ void ikg_collide_continue_kernel(const KModel<T>* __restrict__ m,
   bool success = false, passive_clamped = it > 0;
   T nrm = T(0);
 #ifdef IKG_CPROF
-  unsigned long long prof[4] = {0, 0, 0, 0}, t = clock64(), a_fk = 0, a_up = 0, a_col = 0;
+  unsigned long long prof[5] = {0, 0, 0, 0, 0}, t = clock64(), a_fk = 0, a_up = 0, a_col = 0;
   const int it0 = it;
   bool cp_lead = li == 0 && active;
 #else
@@ -1312,7 +1318,18 @@ __global__ __launch_bounds__(64) void ikg_prescreen_kernel(const KModel<T>* __re
   __syncthreads();
   stage_trig_par(m, S);
   __syncthreads();
+#ifdef IKG_CPROF
+  unsigned long long prof[5] = {0, 0, 0, 0, 0};
+  const bool col = collide_wave<T, true>(m, c, S, tgt, W, prof);
+  if (lane == 0) {  // pre-screen: checks, frames, sweep, of it the sphere pass (tools/scan_prof.py)
+    atomicAdd(&g_scan[24], 1ull);
+    atomicAdd(&g_scan[25], prof[0]);
+    atomicAdd(&g_scan[26], prof[2]);
+    atomicAdd(&g_scan[27], prof[4]);
+  }
+#else
   const bool col = collide_wave<T, true>(m, c, S, tgt, W);
+#endif
   if (lane == 0) witness[p] = col ? W.pair : -1;
 }
 
@@ -1697,7 +1714,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     }
     int ans = -1;
 #ifdef IKG_CPROF
-    unsigned long long sprof[4] = {0, 0, 0, 0}, n_chk = 0, n_lane = 0;
+    unsigned long long sprof[5] = {0, 0, 0, 0, 0}, n_chk = 0, n_lane = 0;
     const unsigned long long st0 = clock64();
     unsigned long long* prof = sprof;
 #else
@@ -2236,7 +2253,7 @@ extern "C" int ikg_debug_wprof(unsigned long long* out, int reset) {
 extern "C" int ikg_debug_scan(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_scan), sizeof(g_scan)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[24] = {};
+    unsigned long long z[28] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_scan), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

@@ -28,7 +28,7 @@ lib = _lib.load()
 lib.ikg_debug_scan.argtypes = [C.c_void_p, C.c_int]
 tdt = torch.float64 if dtype == "f64" else torch.float32
 tg = torch.tensor(uniform_targets(B, seed=0), dtype=tdt, device="cuda")
-buf = np.zeros(24, np.uint64)
+buf = np.zeros(28, np.uint64)
 s.solve(tg, torch.zeros(15, dtype=tdt), check_collision=True)
 torch.cuda.synchronize()
 lib.ikg_debug_scan(buf.ctypes.data, 1)
@@ -44,4 +44,6 @@ print(json.dumps({"batch": B, "dtype": dtype, "problem_windows": n, "checks_max"
                   "cert_cycles_placements": int(buf[12]), "cert_cycles_search": int(buf[13]),
                   "cert_cycles_finish": int(buf[14]), "witness_and_check_cycles": int(buf[15]),
                   "chunk_cert_stage_cycles": int(buf[16]), "passive_fill_cycles": int(buf[17]),
-                  "cover_cycles": int(buf[18]), "cover_calls": int(buf[19])}))
+                  "cover_cycles": int(buf[18]), "cover_calls": int(buf[19]),
+                  "prescreen_checks": int(buf[24]), "prescreen_frames_cycles": int(buf[25]),
+                  "prescreen_sweep_cycles": int(buf[26]), "prescreen_sphere_pass_cycles": int(buf[27])}))
