@@ -4,6 +4,7 @@ import ctypes as C
 import glob
 import os
 import sys
+import zlib
 
 import numpy as np
 import torch
@@ -64,7 +65,9 @@ prm = _lib.Params(eps=float(os.environ.get("ABL_EPS", "1e-37")), dt=1e-2, max_it
                   variant=int(os.environ.get("ABL_VARIANT", "0")), lambda_=0.0, check_collision=int(COL))
 s = torch.cuda.current_stream().cuda_stream
 times = {n: [] for n, _, _ in handles}
-for rnd in range(int(os.environ.get("ABL_ROUNDS", "6"))):
+digest = {}  # outputs of each library's last run: equal digests = bit-identical answers
+NR = int(os.environ.get("ABL_ROUNDS", "6"))
+for rnd in range(NR):
     for n, lib, h in handles:
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         if MS:
@@ -86,5 +89,7 @@ for rnd in range(int(os.environ.get("ABL_ROUNDS", "6"))):
         assert rc == 0
         if rnd > 0:
             times[n].append(a.elapsed_time(b))
+        if rnd == NR - 1:
+            digest[n] = zlib.crc32(b"".join(x.cpu().numpy().tobytes() for x in (qo, cv, it, er)))
 for n, t in times.items():
-    print(f"{n:30s} B={B} {dtype}: median {np.median(t):.3f} ms  min {np.min(t):.3f}  ({np.median(t) / 1000 * 1e3:.2f} us/iter)")
+    print(f"{n:30s} B={B} {dtype}: median {np.median(t):.3f} ms  min {np.min(t):.3f}  ({np.median(t) / 1000 * 1e3:.2f} us/iter)  digest {digest.get(n, 0):08x}")
