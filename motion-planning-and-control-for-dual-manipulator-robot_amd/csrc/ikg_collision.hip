@@ -12,6 +12,7 @@
 //    ~745-pair check.
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
 #include <cstdlib>
 
 #include "ikg_collision.hpp"
@@ -1383,6 +1384,17 @@ static int scan_cert() {
   const char* e = getenv("IKG_SCAN_CERT");
   return e ? atoi(e) : 1;
 }
+// waves of the records scan (grid-stride over the listed problems): one per
+// problem up to 65,536.  The listed count is known only on the device, so the
+// grid is sized by B and waves past it return at once.  A grid of 1,024 (one
+// wave per SIMD, ~8.5 windows each at C3) took C3 + collision 2.21 ms against
+// 1.98 (profiles/r05/collision/scan_waves/); IKG_SCAN_WAVES (read at every
+// launch) sets it for A/Bs
+static int64_t scan_waves(int64_t B) {
+  const char* e = getenv("IKG_SCAN_WAVES");
+  const int64_t w = e ? std::max(1, atoi(e)) : 65536;
+  return std::min<int64_t>(w, B);
+}
 // the record layout (kRec*, rec_len, store_block8) is in ikg_solve.hpp
 
 template <typename T>
@@ -1642,7 +1654,13 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
   __shared__ CollideScratch<T> S;
   __shared__ T tgt[12];
   __shared__ Witness<T> W;
-  __shared__ T PL[64][2][12];  // per-lane witness placements
+  // per-lane witness placements: live only inside a witness round, so they
+  // share S's transform tables (S.L..S.cand), which the certificate (S.L as
+  // its joint table) and the full check (collide_wave) use only between rounds;
+  // 6 KB less LDS per wave in fp32 (17.9 -> 11.7 KB: 3 waves per SIMD)
+  static_assert(offsetof(CollideScratch<T>, cand) + sizeof(S.cand) - offsetof(CollideScratch<T>, L) >=
+                    sizeof(T) * 64 * 2 * 12, "witness placements fit S's transform tables");
+  T(*const PL)[2][12] = reinterpret_cast<T(*)[2][12]>(&S.L[0][0]);
   __shared__ int32_t SL[kMaxNq];  // joint -> record slot
   __shared__ BallCert<T> BC;   // the witness pair's inscribed-ball certificate (ball_cert)
   __shared__ int32_t bc_pair;  // the pair BC certifies (-1: none yet for this problem)
@@ -2184,7 +2202,7 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     poison_int(dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     // one scan round with the pre-screen's witnesses: `done` is only written
     // (read by later rounds, of which there are none here), so it needs no fill
-    hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)std::min<int64_t>(1024, a.B)), dim3(64), 0, s, dm, dc,
+    hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)scan_waves(a.B)), dim3(64), 0, s, dm, dc,
                        (const T*)a.targets, a.S, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
                        (const int32_t*)w.wit, tw, prm.max_iters + 1, 0, (T*)a.q_out, a.converged, a.iters,
                        (T*)a.err_out);
