@@ -137,19 +137,37 @@ __device__ bool collide_wave(const KModel<T>* __restrict__ m, const KCollision<T
   // rounds of 64.  A collision-free pose runs ~2 narrow-phase rounds instead of
   // a GJK-latency round in each of the 12 rounds of 64 pairs; the answer and
   // the witness (lowest colliding pair) are the single pass's.
+  // Every round's pair indices and thresholds are loaded before the first
+  // test (one memory round trip per check instead of two dependent ones per
+  // round of 64 pairs; the thresholds are precomputed per pair, pr2)
   int ncand = 0;
-  for (int base = 0; base < c->n_pairs; base += 64) {
-    const int k = base + lane;
-    bool pass = false;
-    if (k < c->n_pairs && k != w) {
-      const int a = c->pairs[k][0], b = c->pairs[k][1];
-      const T d0 = S.P[a][9] - S.P[b][9], d1 = S.P[a][10] - S.P[b][10], d2 = S.P[a][11] - S.P[b][11];
-      const T r = c->brad[a] + c->brad[b];
-      pass = d0 * d0 + d1 * d1 + d2 * d2 < r * r;
+  {
+    constexpr int kRounds = kMaxPairs / 64;
+    const int np = c->n_pairs;
+    const uint32_t* __restrict__ pw = reinterpret_cast<const uint32_t*>(&c->pairs[0][0]);
+    uint32_t pk[kRounds];
+    T r2[kRounds];
+#pragma unroll
+    for (int i = 0; i < kRounds; ++i) {
+      const int k = i * 64 + lane;
+      const bool in = k < np;
+      pk[i] = in ? pw[k] : 0u;
+      r2[i] = in ? c->pr2[k] : T(0);
     }
-    const unsigned long long bal = __ballot(pass);
-    if (pass) S.cand[ncand + __popcll(bal & ((1ull << lane) - 1))] = (int16_t)k;
-    ncand += __popcll(bal);
+#pragma unroll
+    for (int i = 0; i < kRounds; ++i) {
+      if (i * 64 >= np) break;  // wave-uniform
+      const int k = i * 64 + lane;
+      bool pass = false;
+      if (k < np && k != w) {
+        const int a = (int16_t)(pk[i] & 0xFFFFu), b = (int16_t)(pk[i] >> 16);
+        const T d0 = S.P[a][9] - S.P[b][9], d1 = S.P[a][10] - S.P[b][10], d2 = S.P[a][11] - S.P[b][11];
+        pass = d0 * d0 + d1 * d1 + d2 * d2 < r2[i];
+      }
+      const unsigned long long bal = __ballot(pass);
+      if (pass) S.cand[ncand + __popcll(bal & ((1ull << lane) - 1))] = (int16_t)k;
+      ncand += __popcll(bal);
+    }
   }
   __syncthreads();
 #ifdef IKG_CPROF

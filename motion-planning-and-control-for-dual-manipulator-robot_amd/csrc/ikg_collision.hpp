@@ -29,6 +29,7 @@ struct KCollision {
   int32_t kind[kMaxGeoms];
   int32_t joint[kMaxGeoms];
   int16_t pairs[kMaxPairs][2];
+  T pr2[kMaxPairs];  // per pair: (brad[a] + brad[b])^2, the bounding-sphere test's threshold
   int32_t n_geoms;
   int32_t n_pairs;
   int32_t target_geom;

@@ -215,6 +215,8 @@ inline void build_kcollision(const ikg_collision_desc& d, KCollision<T>& c) {
   for (int k = 0; k < d.n_pairs; ++k) {
     c.pairs[k][0] = (int16_t)d.pairs[k][0];
     c.pairs[k][1] = (int16_t)d.pairs[k][1];
+    const T r = c.brad[d.pairs[k][0]] + c.brad[d.pairs[k][1]];  // as the device would form it
+    c.pr2[k] = r * r;
   }
 }
 
