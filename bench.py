@@ -593,11 +593,12 @@ def main():
                               max_iters=None if (S or args.collision) else max_iters)
         if args.collision:
             # the batch kernel records the run-on iterates when they fit the record budget
-            # (ikg_capi.hip rec_budget: 1 GiB, 20 values per iterate), else the trajectory kernel
-            # recomputes them in windows
-            budget = int(os.environ.get("IKG_REC_BUDGET_MB", "1024")) << 20
+            # in fixed slots when they fit the record budget (ikg_capi.hip rec_budget: 6 GiB,
+            # 20 values per iterate), else in a pool of that size the converged problems reserve
+            # from (a problem that finds it full goes to the trajectory kernel)
+            budget = int(os.environ.get("IKG_REC_BUDGET_MB", "6144")) << 20
             rec_bytes = (8 if args.dtype == "f64" else 4) * 20 * 1001 * B * max(S, 1)
-            if rec_bytes <= budget:
+            if rec_bytes <= budget or os.environ.get("IKG_REC_POOL", "1") != "0":
                 rl["kernel"] = kname + " (records every iterate past the first passing one) + " \
                                        "ikg_prescreen_kernel + ikg_traj_scan_kernel"
                 rl["kernel_ms_covers"] = "the whole solve: batch kernel, pre-screen, compaction, record scan"

@@ -65,8 +65,8 @@
  * Scratch memory
  *   - Uncaptured solves take their scratch from a stream-ordered pool the
  *     model owns (one per device it solves on).  The pool keeps up to
- *     1.25 GiB of freed memory reserved for the next solve (the collision
- *     records are the large item, up to 1 GiB per solve; environment
+ *     6.5 GiB of freed memory reserved for the next solve (the collision
+ *     records are the large item, up to 6 GiB per solve; environment
  *     IKG_WS_KEEP_MB overrides the amount) and releases the rest at the next
  *     synchronisation.  ikg_model_trim synchronises each such device and
  *     releases everything the pools hold unused; ikg_model_destroy

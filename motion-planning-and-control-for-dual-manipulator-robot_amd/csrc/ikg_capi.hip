@@ -232,13 +232,16 @@ static bool rec_in_batch() {
   const char* e = getenv("IKG_TRAJ_REC");
   return !(e && atoi(e) == 0);
 }
-// Budget 1 GiB (C2 fp64: 656 MB).  Larger budgets were measured: C3 fp32's
-// 5.2 GB of packed-kernel records scan in about the time the trajectory
-// windows take (2.21-2.39 against 2.33-2.34 ms), so the memory
-// is not spent.  IKG_REC_BUDGET_MB overrides (measurement knob).
+// Budget 6 GiB, ~2% of an MI355X's 288 GB (C2 fp64: 656 MB fixed slots; C3
+// fp32: 5.2 GB fixed slots).  With one wave per problem in the records scan
+// the fixed slots beat the pool at C3: the pooled records loop carries the
+// reservation state (C3 + collision 1.955 -> 1.842 ms against a 1 GiB pool,
+// profiles/r05/collision/rec_budget/).  Above it (C4 f64 21 GB, C5 10.5 GB)
+// the problems reserve from a pool of this size.  IKG_REC_BUDGET_MB overrides.
+constexpr size_t kRecBudgetMB = 6144;
 static size_t rec_budget() {
   if (const char* e = getenv("IKG_REC_BUDGET_MB")) return (size_t)atoll(e) << 20;
-  return size_t(1) << 30;
+  return kRecBudgetMB << 20;
 }
 
 

@@ -405,15 +405,20 @@ def test_pooled_records_equal_fixed_records(csolver, monkeypatch):
 
 def test_pooled_records_c3_fp32(csolver, monkeypatch):
     """C3 (65,536 fp32, packed layout) with the collision term: its fixed
-    records (5.2 GB) exceed the budget, so the packed kernel records into the
-    pool; against the trajectory kernel for the whole batch (IKG_REC_POOL=0):
+    records (5.2 GB) fit the default 6 GiB budget; under a 1 GiB budget the
+    packed kernel records into the pool instead, with the fixed slots' bits.
+    Against the trajectory kernel for the whole batch (IKG_REC_POOL=0):
     flags and counts agree on >= 99.9% (fp32: the trajectory kernel resyncs
     its trig per window), q to fp32 rounding, deterministic."""
     from ikgrasp.workload import uniform_targets
     tg = uniform_targets(65536, seed=0)
-    a = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
+    f = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)  # fixed slots
+    monkeypatch.setenv("IKG_REC_BUDGET_MB", "1024")
+    a = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)  # pooled
     a2 = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
     assert np.array_equal(a.q, a2.q) and np.array_equal(a.iters, a2.iters)
+    for x, y in zip((f.q, f.converged, f.iters, f.err), (a.q, a.converged, a.iters, a.err)):
+        assert np.array_equal(x, y)
     monkeypatch.setenv("IKG_REC_POOL", "0")
     b = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
     same = (a.converged == b.converged) & (a.iters == b.iters)
