@@ -1739,13 +1739,20 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
 #else
     unsigned long long* pc = nullptr;
 #endif
-    if (w.by_p) {  // the pair kernel records no passive joints: constant from the first update on
-      const T* qo = q_out + p * nq;
+    if (w.by_p) {  // the batch kernels record no passive joints: constant from the first update on
+      // staged in LDS first: read from q_out inside the loop, they were reloaded
+      // after every record store (q_out may alias the records), a memory round
+      // trip per 64 records
+      const int npv = m->n_passive;
+      if (lane < npv) {
+        const int pj = m->passive_q[lane];
+        const T v = q_out[p * nq + pj];
+        S.sn[lane] = v;                                // the first iterate's value (it0 + j = 0)
+        S.cs[lane] = clampq(v, m->lo[pj], m->hi[pj]);  // every later one
+      }
+      __syncthreads();
       for (int j = lane; j < nrec; j += 64)
-        for (int k = 0; k < m->n_passive; ++k) {
-          const int pj = m->passive_q[k];
-          rec[(int64_t)j * RL + kRecPassive + k] = it0 + j > 0 ? clampq(qo[pj], m->lo[pj], m->hi[pj]) : qo[pj];
-        }
+        for (int k = 0; k < npv; ++k) rec[(int64_t)j * RL + kRecPassive + k] = it0 + j > 0 ? S.cs[k] : S.sn[k];
       __syncthreads();
     }
     int ans = -1;
