@@ -1393,6 +1393,10 @@ struct TrajWs {
   int by_p = 0;       // records, counts and it0 indexed by problem (the pair kernel's records)
   const int32_t* rbase = nullptr;  // by_p, pooled records: each problem's first record (ikg_solve.hpp RecPool)
   int cert = 1;       // inscribed-ball certificates before the witness tests (IKG_SCAN_CERT=0: off)
+  // round -2 (records, no separate pre-screen): problem i = index i of the
+  // batch, every converged one checked first; wit_out[i] = the colliding pair
+  // found, -1 if none or not converged
+  int32_t* wit_out = nullptr;
 };
 
 // IKG_SCAN_CERT=0: the records scan without inscribed-ball certificates (A/B
@@ -1408,6 +1412,17 @@ static int scan_cert() {
 // wave per SIMD, ~8.5 windows each at C3) took C3 + collision 2.21 ms against
 // 1.98 (profiles/r05/collision/scan_waves/); IKG_SCAN_WAVES (read at every
 // launch) sets it for A/Bs
+// With records, the first check and the records scan of a problem in one wave
+// of one launch (traj_scan_body round -2) instead of the pre-screen, the
+// compaction and a scan over the listed problems: C2 + collision 1.212 ->
+// 1.199 ms, C3 + collision 1.807 -> 1.800, but C5 + collision (131,072
+// problems per launch) 3.502 -> 3.574 (profiles/r05/collision/prescan/), so
+// up to 65,536 problems per launch.  IKG_PRESCAN=0/1 (read at every launch)
+// forces either form.
+static bool prescan_on(int64_t B) {
+  const char* e = getenv("IKG_PRESCAN");
+  return e ? atoi(e) != 0 : B <= 65536;
+}
 static int64_t scan_waves(int64_t B) {
   const char* e = getenv("IKG_SCAN_WAVES");
   const int64_t w = e ? std::max(1, atoi(e)) : 65536;
@@ -1691,7 +1706,12 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     // answered by an earlier scan: window r - 1's, or (no pre-screen: witness0
     // null) the first checks' before window 0
     if ((round > 0 || (round == 0 && !witness0)) && w.done[i]) continue;  // wave-uniform
-    const int64_t p = clist[i];
+    const bool fused = round == -2;  // first check, then (colliding) this problem's records
+    const int64_t p = fused ? (int64_t)i : (int64_t)clist[i];
+    if (fused && !conv[p]) {  // wave-uniform
+      if (lane == 0) w.wit_out[p] = -1;
+      continue;
+    }
     const int64_t t_idx = S_per_target > 1 ? p / S_per_target : p;
     if (lane < 12) tgt[lane] = targets[t_idx * 12 + lane];
     if (lane < nq) S.par[lane] = m->jparent[lane];
@@ -1709,13 +1729,15 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       __syncthreads();
       const bool col = collide_wave<T, true>(m, c, S, tgt, W);
       if (lane == 0) {
-        if (col)
+        if (fused)
+          w.wit_out[p] = col ? W.pair : -1;
+        else if (col)
           w.cst[i].pair = W.pair;
         else
           w.done[i] = 1;  // :70 errors pass and no collision: final as the batch kernel left it
       }
       __syncthreads();
-      continue;
+      if (!(fused && col)) continue;  // wave-uniform; fused + colliding: scan the records with this witness
     }
     const int64_t ix = w.by_p ? p : par + i;
     const int nr = w.nrec[ix];
@@ -1924,8 +1946,8 @@ void ikg_traj_scan_kernel(const KModel<T>* __restrict__ m,
                                                            const int32_t* __restrict__ witness0, TrajWs<T> w, int Wn,
                                                            int r, T* __restrict__ q_out, uint8_t* __restrict__ conv,
                                                            int32_t* __restrict__ iters, T* __restrict__ err) {
-  traj_scan_body<T>(m, c, targets, S_per_target, clist, *count, witness0, w, Wn, r, q_out, conv, iters, err,
-                    (int)blockIdx.x, (int)gridDim.x);
+  traj_scan_body<T>(m, c, targets, S_per_target, clist, count ? *count : (int)w.slots, witness0, w, Wn, r, q_out,
+                    conv, iters, err, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // Launch r of rounds + 1: window r's updates on the first `tblocks`
@@ -2195,13 +2217,16 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
   // trajectory continuation without a pre-screen: the first checks run in its
   // first launch, so every converged problem is listed
   const bool first = !(a.rec_used && *a.rec_used) && cont_traj(a.B) && !traj_prescreen(a.B);
-  if (first)
+  const bool fused = a.rec_used && *a.rec_used && prescan_on(a.B);
+  if (fused) {
+    // nothing here: the scan below checks every converged problem itself
+  } else if (first)
     hipLaunchKernelGGL(ikg_mark_converged_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s,
                        (const uint8_t*)a.converged, a.B, w.wit);
   else
     hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
                        (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
-  {  // the chunk counts borrow the stretch list (written only after the compaction)
+  if (!fused) {  // the chunk counts borrow the stretch list (written only after the compaction)
     const unsigned nb = (unsigned)((a.B + kCompactChunk - 1) / kCompactChunk);
     hipLaunchKernelGGL(ikg_compact_count_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)w.wit, a.B, w.list);
     hipLaunchKernelGGL(ikg_compact_write_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)w.wit, a.B,
@@ -2227,10 +2252,18 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     poison_int(dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     // one scan round with the pre-screen's witnesses: `done` is only written
     // (read by later rounds, of which there are none here), so it needs no fill
-    hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)scan_waves(a.B)), dim3(64), 0, s, dm, dc,
-                       (const T*)a.targets, a.S, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
-                       (const int32_t*)w.wit, tw, prm.max_iters + 1, 0, (T*)a.q_out, a.converged, a.iters,
-                       (T*)a.err_out);
+    if (fused) {  // one wave per problem of the batch: its first check, then its records if it collides
+      tw.wit_out = w.wit;
+      hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)std::min<int64_t>(a.B, int64_t(1) << 20)), dim3(64),
+                         0, s, dm, dc, (const T*)a.targets, a.S, (const int32_t*)nullptr, (const int32_t*)nullptr,
+                         (const int32_t*)nullptr, tw, prm.max_iters + 1, -2, (T*)a.q_out, a.converged, a.iters,
+                         (T*)a.err_out);
+    } else {
+      hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)scan_waves(a.B)), dim3(64), 0, s, dm, dc,
+                         (const T*)a.targets, a.S, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
+                         (const int32_t*)w.wit, tw, prm.max_iters + 1, 0, (T*)a.q_out, a.converged, a.iters,
+                         (T*)a.err_out);
+    }
     ec = hipGetLastError();
     ws_trace("free scan", dws, 0, s);
     const hipError_t ef2 = ws_free(a.ws_owner, dws, s);
