@@ -293,6 +293,43 @@ def roofline(dtype, kernel, med, kern_ms, sum_iters, waves, simds, abytes, traff
     return out, hbm
 
 
+def iters_hist(iters, max_iters=1000, width=50):
+    """Update-count histogram (SURVEY §5 "Metrics"; the reference's own
+    convergence evidence is per-iteration charts, inverse_geometry_TESTS.py:403-450):
+    50-update bins [lo, lo + 49] below max_iters, and the max_iters bucket (the
+    loop exhausted: not converged, or converged-but-colliding that ran on)."""
+    it = np.asarray(iters).astype(np.int64).ravel()
+    h = {}
+    for lo in range(0, max_iters, width):
+        h[f"{lo}-{min(lo + width, max_iters) - 1}"] = int(((it >= lo) & (it < lo + width) & (it < max_iters)).sum())
+    h[str(max_iters)] = int((it >= max_iters).sum())
+    return h
+
+
+REC_BUDGET_MB = 6144  # ikg_capi.hip kRecBudgetMB (IKG_REC_BUDGET_MB overrides)
+
+
+def collision_kernels(kname, dtype, B, S=0):
+    """The kernels a collision solve runs, by the C-ABI's rules
+    (ikg_capi.hip rec_chunk, ikg_collision.hip prescan_on): the batch kernel
+    with records in launches whose fixed record slots fit the budget, then per
+    launch either the first check fused into the records scan (up to 65,536
+    problems per launch, IKG_PRESCAN) or pre-screen + compaction + scan."""
+    slot = (8 if dtype == "f64" else 4) * 20 * 1001 * max(S, 1)  # one unit's records (a target's S seeds)
+    budget = int(os.environ.get("IKG_REC_BUDGET_MB", str(REC_BUDGET_MB))) << 20
+    cap = max(1, budget // slot)
+    chunks = 1 if B <= cap else -(-B // cap)
+    per = -(-B // chunks) * max(S, 1)  # problems per launch
+    pre = os.environ.get("IKG_PRESCAN")
+    fused = (int(pre) != 0) if pre is not None else per <= 65536
+    label = kname + " (records every iterate past the first passing one) + " + (
+        "ikg_traj_scan_kernel (first check fused with the records scan)" if fused else
+        "ikg_prescreen_kernel + ikg_compact_count_kernel + ikg_compact_write_kernel + ikg_traj_scan_kernel")
+    if chunks > 1:
+        label += f"; {chunks} launch sequences of {per} problems (records budget {budget >> 20} MB)"
+    return label, "the whole solve (all its kernels)"
+
+
 # ---------------------------------------------------------------- launcher
 def _free_port():
     with socket.socket() as s:
@@ -550,6 +587,7 @@ def main():
     n_conv = int(conv.sum().item())
     sum_iters = int(iters.to(torch.int64).sum().item())
     max_iters = int(iters.max().item()) if B else 0
+    hist = iters_hist(iters.cpu().numpy())
     if S:
         # the multi-start launch returns the winner's update count only; its per-seed solves are
         # exactly ikg_solve_batch over the expanded (target, seed) problems (same kernel, same
@@ -565,6 +603,7 @@ def main():
                           check_collision=args.collision)
         torch.cuda.synchronize()
         sum_iters = int(i_x.to(torch.int64).sum().item())
+        hist = iters_hist(i_x.cpu().numpy())
         del tg_x, q0_x, q_x, c_x, i_x, e_x
     elapsed, kern_ms, tot_conv, tot_B, tot_iters = reduce_stats(
         torch, dist, world, host, dev, [elapsed, kern_ms, n_conv, B, sum_iters], 2)
@@ -592,20 +631,7 @@ def main():
                               -(-B * max(S, 1) // ppw), cus * 4, abytes, traffic, tsrc,
                               max_iters=None if (S or args.collision) else max_iters)
         if args.collision:
-            # the batch kernel records the run-on iterates when they fit the record budget
-            # in fixed slots when they fit the record budget (ikg_capi.hip rec_budget: 6 GiB,
-            # 20 values per iterate), else in a pool of that size the converged problems reserve
-            # from (a problem that finds it full goes to the trajectory kernel)
-            budget = int(os.environ.get("IKG_REC_BUDGET_MB", "6144")) << 20
-            rec_bytes = (8 if args.dtype == "f64" else 4) * 20 * 1001 * B * max(S, 1)
-            if rec_bytes <= budget or os.environ.get("IKG_REC_POOL", "1") != "0":
-                rl["kernel"] = kname + " (records every iterate past the first passing one) + " \
-                                       "ikg_prescreen_kernel + ikg_traj_scan_kernel"
-                rl["kernel_ms_covers"] = "the whole solve: batch kernel, pre-screen, compaction, record scan"
-            else:
-                rl["kernel"] = kname + " + ikg_prescreen_kernel + ikg_traj_kernel (the run-on iterates " \
-                                       "recomputed and scanned in windows: records exceed the budget)"
-                rl["kernel_ms_covers"] = "the whole solve: batch kernel, pre-screen, compaction, trajectory windows"
+            rl["kernel"], rl["kernel_ms_covers"] = collision_kernels(kname, args.dtype, B, S)
         else:
             rl["kernel"] = kname
         parallelism = f"shard{world}"
@@ -633,6 +659,9 @@ def main():
             "converged_fraction": tot_conv / tot_B,
             "mean_iters": (tot_iters / tot_B) if not S else None,
             "mean_iters_all_problems": (tot_iters / (tot_B * S)) if S else None,
+            "iters_hist": hist,
+            "iters_hist_is": ("update counts of every (target, seed) problem of rank 0's launch" if S else
+                              "update counts of rank 0's batch") + " (50-update bins; '1000': the loop exhausted)",
             "roofline": rl,
             "roofline_hbm": rl_hbm,
             "ranks": rank_block(per, world, backend, gather_ms,
@@ -640,6 +669,10 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline and not S and not args.collision:
             out["cpu_baseline"] = cpu_baseline(tg_np)
+        if "c2_collision" in extra:  # the reference's success (collision term) beside the headline's
+            out["value_with_collision"] = extra["c2_collision"]["value"]
+            out["value_with_collision_is"] = ("extra.c2_collision: collision-free converged solves/s, the "
+                                              "reference's success (inverse_geometry.py:70, :97-98)")
         if extra:
             if world == 1 and not args.no_cpu_baseline and "c2_collision" in extra:
                 extra["c2_collision"]["cpu_baseline"] = cpu_baseline_collision(tg_np, solver.scene.to_json())
@@ -684,6 +717,7 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
     steps4 = max(3, min(args.steps, 5))
     el4, km4_local = timed(torch, dist, world, steps4, 1, step4, stream)
     it4_local = int(i4.to(torch.int64).sum().item())
+    hist4 = iters_hist(i4.cpu().numpy())
     per4 = per_rank(torch, dist, world, host, dev, [km4_local])
     g4 = time_collective(torch, dist, world, gather4)
     el4, km4, conv4, it4 = reduce_stats(torch, dist, world, host, dev,
@@ -704,6 +738,7 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
             "value": conv4 / ps, "unit": "converged solves/s", "problems_per_s": tot / ps,
             "ms_per_step": ps * 1e3, "kernel_ms_max_rank": km4, "scaling": "strong", "n_gpus": world,
             "steps": steps4, "converged_fraction": conv4 / tot,
+            "iters_hist": hist4, "iters_hist_is": "rank 0's shard",
             "roofline": rl4, "roofline_hbm": rl4_hbm,
             "ranks": rank_block(per4, world, "nccl" if not host else "gloo", g4,
                                 "blocking gather_rows of q, flags and update counts of the whole batch to rank 0, "
@@ -734,9 +769,7 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
         traffic, tsrc = hbm_profile("f64", B, 0, True)
         rl, rl_hbm = roofline("f64", "pair", False, kmc, int(itc), -(-B // 32), cus * 4,
                               algorithmic_bytes("f64", B) + 48 * 8 * 12, traffic, tsrc)
-        rl["kernel"] = ("ikg_pair_batch_kernel (records every iterate past the first passing one) + "
-                        "ikg_prescreen_kernel + ikg_traj_scan_kernel")
-        rl["kernel_ms_covers"] = "the whole solve (all its kernels)"
+        rl["kernel"], rl["kernel_ms_covers"] = collision_kernels("ikg_pair_batch_kernel", "f64", B)
         rl["work"] += " -- the updates the reference runs; checks are not priced"
         extra["c2_collision"] = {
             "workload": f"BASELINE configs[1] with the reference's success (collision term, "
@@ -744,6 +777,7 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
             "value": convc / ps, "unit": "collision-free converged solves/s", "ms_per_step": ps * 1e3,
             "kernel_ms": kmc, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "converged_fraction": convc / (B * world), "mean_iters": itc / (B * world),
+            "iters_hist": iters_hist(ic.cpu().numpy()),
             "roofline": rl, "roofline_hbm": rl_hbm,
         }
     # ---- C2 with random yaw: the "random SE(3)" reading of configs[1] (the
@@ -762,6 +796,7 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
     ely, kmy_local = timed(torch, dist, world, args.steps, args.warmup, stepy, stream)
     ity_local = int(ic.to(torch.int64).sum().item())
     ity_max = int(ic.max().item())
+    hist_y = iters_hist(ic.cpu().numpy())
     ely, kmy, convy, ity = reduce_stats(torch, dist, world, host, dev,
                                         [ely, kmy_local, int(cc.sum().item()), ity_local], 2)
     if rank == 0:
@@ -777,6 +812,7 @@ def run_extras(torch, dist, world, rank, host, dev, solver, code, tdt, args, str
             "value": convy / ps, "unit": "converged solves/s", "ms_per_step": ps * 1e3, "kernel_ms": kmy,
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "converged_fraction": convy / (B * world), "mean_iters": ity / (B * world),
+            "iters_hist": hist_y,
             "roofline": rl, "roofline_hbm": rl_hbm,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -30,13 +30,19 @@
  *     the last failure on the calling thread is ikg_last_error().  Nothing
  *     throws or exits across this boundary.
  *   - Calls are re-entrant per (model, stream).
- *   - Results are deterministic.  A problem's fp64 answer is the same bit for
- *     bit in any batch size and batch position, with two exceptions.  With
- *     the collision term, a problem that converges into collision runs on in
- *     the batch kernel itself (records) when the batch's records fit the
- *     record budget, else in the trajectory kernel, which resyncs the joint
- *     sin/cos per window: the two agree to rounding (q <= 1e-9), and which
- *     one runs depends on the batch size.  And in fp64 a broadcast q0
+ *   - Results are deterministic: no answer depends on the order in which a
+ *     launch's waves run.  A problem's fp64 answer is the same bit for bit in
+ *     any batch size and batch position, with one exception below.  With the
+ *     collision term, a problem that converges into collision runs on in the
+ *     batch kernel itself, which records every later iterate into the
+ *     problem's own fixed slot; a batch whose records exceed the record
+ *     budget (IKG_REC_BUDGET_MB, 6 GiB) is solved as several launches of
+ *     equal size whose records fit, every launch in the layout the whole
+ *     batch would take, so the answer is the one-launch answer.  (Models the
+ *     batch kernel does not record for -- generic or run-time-compiled
+ *     kernels, lambda > 0, the QUAD layout -- run on in the trajectory
+ *     kernel, which agrees with the records to rounding, q <= 1e-9.)  And in
+ *     fp64 a broadcast q0
  *     (q0_stride = 0) and per-problem q0 rows (and multi-start seeds)
  *     advance the joint sin/cos by different rules for steps of
  *     0.025..0.25 rad (exact sincos / a longer series), so when such steps

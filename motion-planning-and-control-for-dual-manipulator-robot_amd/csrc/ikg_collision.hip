@@ -1391,7 +1391,6 @@ struct TrajWs {
   TrajCert<T>* cst;
   int64_t slots;      // slots per parity
   int by_p = 0;       // records, counts and it0 indexed by problem (the pair kernel's records)
-  const int32_t* rbase = nullptr;  // by_p, pooled records: each problem's first record (ikg_solve.hpp RecPool)
   int cert = 1;       // inscribed-ball certificates before the witness tests (IKG_SCAN_CERT=0: off)
   // round -2 (records, no separate pre-screen): problem i = index i of the
   // batch, every converged one checked first; wit_out[i] = the colliding pair
@@ -1741,16 +1740,10 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     }
     const int64_t ix = w.by_p ? p : par + i;
     const int nr = w.nrec[ix];
-    // the record pool was full when it converged: the trajectory kernel takes it
-    // (launch_collide_continue); wave-uniform
-    if (nr & kTrajNoRec) {
-      __syncthreads();
-      continue;
-    }
     const int nrec = nr & ~kTrajEnded;
     const bool ended = (nr & kTrajEnded) != 0;
     const int it0 = w.it0[ix];
-    T* rec = w.rec + (w.rbase ? (int64_t)w.rbase[p] * RL : ix * Wn * RL);
+    T* rec = w.rec + ix * Wn * RL;
 #ifdef IKG_CPROF
     // per-window counters, flushed once at the window's end (atomics inside the
     // loop would make the next load wait on them): 0 certificates, 1 positive,
@@ -2157,16 +2150,6 @@ static hipError_t launch_traj_t(const KModel<T>* dm, const KCollision<T>* dc, co
 }
 
 
-// Pooled records: the problems the pre-screen left colliding whose record
-// reservation found the pool full (kTrajNoRec) -- listed for the trajectory
-// continuation (marker >= 0: the pre-screen's witness)
-__global__ __launch_bounds__(256) void ikg_mark_norec_kernel(const int32_t* __restrict__ wit,
-                                                             const int32_t* __restrict__ nrec, int64_t B,
-                                                             int32_t* __restrict__ mark) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < B) mark[i] = (wit[i] >= 0 && (nrec[i] & kTrajNoRec)) ? wit[i] : -1;
-}
-
 // listed for the trajectory continuation without a pre-screen: every problem
 // whose errors passed in the batch kernel (marker >= 0 for the compaction)
 __global__ __launch_bounds__(256) void ikg_mark_converged_kernel(const uint8_t* __restrict__ conv, int64_t B,
@@ -2247,7 +2230,6 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     tw.slots = a.B;
     tw.by_p = 1;
     tw.cert = scan_cert();
-    tw.rbase = a.rec_pool.base;
     ws_trace("alloc scan", dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     poison_int(dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
     // one scan round with the pre-screen's witnesses: `done` is only written
@@ -2268,29 +2250,6 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     ws_trace("free scan", dws, 0, s);
     const hipError_t ef2 = ws_free(a.ws_owner, dws, s);
     if (ec == hipSuccess) ec = ef2;
-    if (ec == hipSuccess && a.rec_pool.cursor) {
-      // pooled records: the colliding problems that found the pool full go
-      // through the interleaved continuation, which needs no record buffers
-      // (the list is empty in the usual case, and the launch's waves then
-      // return at once)
-      const size_t b3 = 3 * ib + 256;
-      char* fws = nullptr;
-      ec = ws_alloc(a.ws_owner, (void**)&fws, b3, s);
-      if (ec != hipSuccess) return ec;
-      poison_int(fws, b3, s);
-      ContWs<T> w2{(int32_t*)w.wit, (int32_t*)fws, (int32_t*)(fws + 3 * ib), (int32_t*)(fws + 2 * ib), w.rec};
-      int32_t* mark = (int32_t*)(fws + ib);
-      hipLaunchKernelGGL(ikg_mark_norec_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s,
-                         (const int32_t*)w.wit, (const int32_t*)a.rec_n, a.B, mark);
-      const unsigned nb = (unsigned)((a.B + kCompactChunk - 1) / kCompactChunk);
-      hipLaunchKernelGGL(ikg_compact_count_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)mark, a.B, w2.list);
-      hipLaunchKernelGGL(ikg_compact_write_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)mark, a.B,
-                         (const int32_t*)w2.list, w2.clist, w2.count + 1);
-      launch_continue_t<T, false, SpecNextage>(dm, dc, prm, a, nq, ng, w2, s);
-      ec = hipGetLastError();
-      const hipError_t ef3 = ws_free(a.ws_owner, fws, s);
-      if (ec == hipSuccess) ec = ef3;
-    }
   } else if (spec == kSpecNextage) {
     if (damped)
       launch_continue_sel<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, w, s, ec, first);

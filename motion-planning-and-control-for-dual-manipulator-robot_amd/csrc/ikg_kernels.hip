@@ -45,7 +45,7 @@ namespace ikg {
 template <typename T, bool DAMPED, class SP>
 constexpr int kPairMinWaves = (kFrame1<SP> && !DAMPED) ? (sizeof(T) == 8 ? 2 : 4) : 1;
 
-template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false, bool POOL = false>
+template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
 __global__ __launch_bounds__(64)
 #if IKG_WPE
 __attribute__((amdgpu_waves_per_eu(1, IKG_WPE)))
@@ -59,12 +59,12 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             uint8_t* __restrict__ conv_out,
                                                             int32_t* __restrict__ iters_out,
                                                             T* __restrict__ err_out, T* __restrict__ rec = nullptr,
-                                                            int32_t* __restrict__ rec_n = nullptr, RecPool pool = {}) {
+                                                            int32_t* __restrict__ rec_n = nullptr) {
   // model tables stay in global memory: the compiler hoists them into
   // registers (staging them in LDS and re-reading per iteration measured 8%
   // slower)
-  pair_batch_body<T, DAMPED, SP, MED, REC, POOL>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
-                                           err_out, rec, rec_n, pool);
+  pair_batch_body<T, DAMPED, SP, MED, REC>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
+                                           err_out, rec, rec_n);
 }
 
 
@@ -238,19 +238,16 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
         (void)launch_pair_ilp(dmodel, prm, a, med, lds_pad_bytes(), s);
         return;
       }
-    if (a.rec) {  // collision continuation records (ikg_collision.hip): fixed slots or the pool
+    if (a.rec) {  // collision continuation records (ikg_collision.hip), one fixed slot per problem
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(64), lds_pad_bytes(), s, dmodel, prm, (const T*)a.targets,
                            (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out, a.converged, a.iters,
-                           (T*)a.err_out, (T*)a.rec, a.rec_n, a.rec_pool);
+                           (T*)a.err_out, (T*)a.rec, a.rec_n);
       };
-      const bool pool = a.rec_pool.cursor != nullptr;
       if (med)
-        pool ? go(ikg_pair_batch_kernel<T, DAMPED, SP, true, true, true>)
-             : go(ikg_pair_batch_kernel<T, DAMPED, SP, true, true, false>);
+        go(ikg_pair_batch_kernel<T, DAMPED, SP, true, true>);
       else
-        pool ? go(ikg_pair_batch_kernel<T, DAMPED, SP, false, true, true>)
-             : go(ikg_pair_batch_kernel<T, DAMPED, SP, false, true, false>);
+        go(ikg_pair_batch_kernel<T, DAMPED, SP, false, true>);
       if (a.rec_used) *a.rec_used = true;
       return;
     }
@@ -314,22 +311,32 @@ static int64_t quad_max_batch() {
   return (int64_t)v;
 }
 
+// The layout a launch of B problems runs (AUTO resolved; PAIR also stands for
+// the generic, damped and model-specialised pair kernels).  The C-ABI fixes it
+// from the whole batch before splitting a collision solve into record chunks
+// (ikg_capi.hip), so every chunk runs the layout the batch would.
+template <typename T>
+int resolve_variant(const KParams<T>& prm, int spec, int variant, int64_t B, bool rec) {
+  if (variant == IKG_VARIANT_QUAD || (variant == IKG_VARIANT_AUTO && B <= quad_max_batch()))
+    if (quad_applies(prm, spec)) return IKG_VARIANT_QUAD;
+  if constexpr (std::is_same<T, float>::value) {
+    static const bool rec_pair = getenv("IKG_REC_PREFER_PAIR") && atoi(getenv("IKG_REC_PREFER_PAIR")) != 0;
+    const bool want = variant == IKG_VARIANT_PACKED ||
+                      (variant == IKG_VARIANT_AUTO && B >= packed_min_batch() && !(rec_pair && rec));
+    if (want && packed_applies(prm, spec)) return IKG_VARIANT_PACKED;
+  }
+  return IKG_VARIANT_PAIR;
+}
+
 template <typename T>
 hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,
                              hipStream_t s) {
   if (a.B <= 0) return hipSuccess;
-  if (a.variant == IKG_VARIANT_QUAD || (a.variant == IKG_VARIANT_AUTO && a.B <= quad_max_batch())) {
-    if (quad_applies(prm, spec)) return launch_quad_batch<T>(dmodel, prm, a, s);
-    if (a.variant == IKG_VARIANT_QUAD) return hipErrorInvalidValue;  // checked by the C-ABI first
-  }
-  if constexpr (std::is_same<T, float>::value) {
-    static const bool rec_pair = getenv("IKG_REC_PREFER_PAIR") && atoi(getenv("IKG_REC_PREFER_PAIR")) != 0;
-    const bool want = a.variant == IKG_VARIANT_PACKED ||
-                      (a.variant == IKG_VARIANT_AUTO && a.B >= packed_min_batch() && !(rec_pair && a.rec));
-    if (want && packed_applies(prm, spec)) {
-      return launch_packed_batch(dmodel, prm, a, s);
-    }
-  }
+  const int v = resolve_variant(prm, spec, a.variant, a.B, a.rec != nullptr);
+  if (v == IKG_VARIANT_QUAD) return launch_quad_batch<T>(dmodel, prm, a, s);
+  if (a.variant == IKG_VARIANT_QUAD) return hipErrorInvalidValue;  // checked by the C-ABI first
+  if constexpr (std::is_same<T, float>::value)
+    if (v == IKG_VARIANT_PACKED) return launch_packed_batch(dmodel, prm, a, s);
   if (a.variant == IKG_VARIANT_PACKED) return hipErrorInvalidValue;  // checked by the C-ABI first
   const bool damped = prm.lambda > T(0);
   if (a.jit) {  // the pair loop compiled against this model's constant tables (ikg_jit.hip)
@@ -375,18 +382,30 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   b.jit = a.jit;
   b.rec = a.rec;
   b.rec_n = a.rec_n;
-  b.rec_pool = a.rec_pool;
   b.rec_used = a.rec_used;
   // AUTO keeps the pair layout here: seeds spread the update counts, and a
   // wave lasts as long as its slowest problem -- 64 per packed wave against 32
   // per pair wave measured 4.17 ms against 3.66 ms (256 seeds x 512 targets,
   // fp32, tools/probe/bisect_c5_trace.sh)
   b.variant = a.variant == IKG_VARIANT_AUTO ? IKG_VARIANT_PAIR : a.variant;
-  hipError_t e = launch_pair_batch<T>(dmodel, prm, b, spec, s);
-  if (e != hipSuccess) return e;
-  if (a.collision) {  // converged-but-colliding seeds keep iterating (inverse_geometry.py:70)
-    e = launch_collide_continue<T>(dmodel, (const KCollision<T>*)a.collision, prm, b, spec, a.nq, a.n_geoms, s);
+  // with collision records: rec_chunk targets (and their S seeds) per launch,
+  // so the records' fixed slots fit the budget (ikg_capi.hip rec_chunk)
+  const int64_t tc = a.rec && a.rec_chunk > 0 ? a.rec_chunk : a.T;
+  for (int64_t t0 = 0; t0 < a.T; t0 += tc) {
+    BatchArgs c = b;
+    const int64_t nt = std::min(tc, a.T - t0);
+    c.B = nt * a.S;
+    c.targets = (const T*)a.targets + t0 * 12;
+    c.q_out = (T*)a.ws_q + t0 * a.S * a.nq;
+    c.converged = a.ws_conv + t0 * a.S;
+    c.iters = a.ws_iters + t0 * a.S;
+    c.err_out = (T*)a.ws_err + t0 * a.S * 2;
+    hipError_t e = launch_pair_batch<T>(dmodel, prm, c, spec, s);
     if (e != hipSuccess) return e;
+    if (a.collision) {  // converged-but-colliding seeds keep iterating (inverse_geometry.py:70)
+      e = launch_collide_continue<T>(dmodel, (const KCollision<T>*)a.collision, prm, c, spec, a.nq, a.n_geoms, s);
+      if (e != hipSuccess) return e;
+    }
   }
   // 2) one wave per target picks the best seed
   const int block = 256;
@@ -434,6 +453,8 @@ template hipError_t launch_pair_batch<double>(const KModel<double>*, const KPara
                                               hipStream_t);
 template hipError_t launch_pair_batch<float>(const KModel<float>*, const KParams<float>&, const BatchArgs&, int,
                                              hipStream_t);
+template int resolve_variant<double>(const KParams<double>&, int, int, int64_t, bool);
+template int resolve_variant<float>(const KParams<float>&, int, int, int64_t, bool);
 template hipError_t launch_multistart<double>(const KModel<double>*, const KParams<double>&, const MultiArgs&, int,
                                               hipStream_t);
 template hipError_t launch_multistart<float>(const KModel<float>*, const KParams<float>&, const MultiArgs&, int,

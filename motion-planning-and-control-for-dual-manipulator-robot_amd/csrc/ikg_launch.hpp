@@ -271,7 +271,6 @@ struct BatchArgs {
   void* rec = nullptr;
   int32_t* rec_n = nullptr;
   bool* rec_used = nullptr;
-  RecPool rec_pool = {};        // pooled records (ikg_solve.hpp RecPool), cursor null: fixed slots
   WsOwner* ws_owner = nullptr;  // scratch of captured solves (ws_alloc)
 };
 
@@ -302,7 +301,7 @@ struct MultiArgs {
   void* rec = nullptr;
   int32_t* rec_n = nullptr;
   bool* rec_used = nullptr;
-  RecPool rec_pool = {};
+  int64_t rec_chunk = 0;  // targets per launch when the records of all T x S problems exceed the budget (0: all)
 };
 
 // Debug knob IKG_POISON=1 (read per call): every stream-ordered workspace is
@@ -342,6 +341,10 @@ constexpr int kSpecGenericWrist = 2;  // generic tables, spherical-wrist solve
 template <typename T>
 hipError_t launch_pair_batch(const KModel<T>* dmodel, const KParams<T>& prm, const BatchArgs& a, int spec,
                              hipStream_t s);
+
+// the concrete layout (IKG_VARIANT_PAIR / PACKED / QUAD) launch_pair_batch runs for B problems
+template <typename T>
+int resolve_variant(const KParams<T>& prm, int spec, int variant, int64_t B, bool rec);
 
 // pair layout, Nextage specialisation, lambda = 0, built with the max-ILP
 // scheduler for launches of at most one wave per SIMD (ikg_pair_ilp.hip)

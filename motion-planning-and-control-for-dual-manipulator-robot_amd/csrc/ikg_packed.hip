@@ -34,7 +34,7 @@ namespace ikg {
 // REC: the collision continuation's records (ikg_collision.hip §3b), written
 // from the first passing iterate on, both arms' blocks by the problem's lane;
 // the outputs at that iterate come from its record 0 (solve_pair).
-template <class SP, int WPS, bool MED, bool REC = false, bool POOL = false>
+template <class SP, int WPS, bool MED, bool REC = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPS == 0 ? 3 : WPS)))
 void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               KParams<float> prm, const float* __restrict__ targets,
@@ -43,7 +43,7 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               uint8_t* __restrict__ conv_out,
                                                               int32_t* __restrict__ iters_out,
                                                               float* __restrict__ err_out, float* __restrict__ rec = nullptr,
-                                                              int32_t* __restrict__ rec_n = nullptr, RecPool pool = {}) {
+                                                              int32_t* __restrict__ rec_n = nullptr) {
   if constexpr (WPS == 1) asm volatile("" ::: "a255");
   // v171: at least 172 VGPRs, so 2 waves fit and 3 do not; an AGPR claim
   // instead makes the allocator split the 2-wave budget 128 VGPR / 128 AGPR
@@ -64,15 +64,10 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
   v2f nrm, other;
   if constexpr (REC) {
     const int rl = rec_len(m->n_passive);
-    RecOut<float> ro{POOL ? rec : rec + p * (int64_t)(prm.max_iters + 1) * rl, rec_n + p, qrow,
+    RecOut<float> ro{rec + p * (int64_t)(prm.max_iters + 1) * rl, rec_n + p, qrow,
                      q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl};
-    if constexpr (POOL) {
-      ro.pool = pool;
-      ro.pool.base = pool.base + p;
-      pool.base[p] = -1;
-    }
     rec_n[p] = 0;
-    if (solve_pair<v2f, false, SP, MED, true, POOL>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
+    if (solve_pair<v2f, false, SP, MED, true>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
     solve_pair<v2f, false, SP, MED>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
   }
@@ -124,7 +119,7 @@ static unsigned simd_count() {
 
 // The cap instantiation really fits WPS waves per SIMD (4 WPS single-wave
 // workgroups per CU) on this device; otherwise the uncapped kernel runs.
-template <int WPS, bool REC = false, bool POOL = false>
+template <int WPS, bool REC = false>
 static bool capped_ok() {
   constexpr int kDevs = 64;
   static std::atomic<int> cache[kDevs];  // 0 unknown, 1 ok, 2 not
@@ -134,7 +129,7 @@ static bool capped_ok() {
   if (!v) {
     int blocks = 0;
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, true, REC, POOL>), 64, packed_lds_pad());
+        &blocks, reinterpret_cast<const void*>(ikg_packed_batch_kernel<SpecNextage, WPS, true, REC>), 64, packed_lds_pad());
     v = (e == hipSuccess && blocks == 4 * WPS) ? 1 : 2;
     cache[dev].store(v, std::memory_order_relaxed);
   }
@@ -149,25 +144,18 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, grid, dim3(64), packed_lds_pad(), s, dmodel, prm, (const float*)a.targets,
                        (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out, a.converged, a.iters,
-                       (float*)a.err_out, (float*)a.rec, a.rec_n, a.rec_pool);
+                       (float*)a.err_out, (float*)a.rec, a.rec_n);
   };
 #ifndef IKG_PACKED_REC
 #define IKG_PACKED_REC 1
 #endif
   if (IKG_PACKED_REC && a.rec) {  // collision continuation records (0: A/B knob, the trajectory kernel instead)
-    auto rec = [&](auto pool) {  // fixed slots or the pool (solve_pair POOL)
-      constexpr bool P = decltype(pool)::value;
-      if (need == 1 && capped_ok<1, true, P>())
-        go(ikg_packed_batch_kernel<SpecNextage, 1, true, true, P>);
-      else if (need == 2 && capped_ok<2, true, P>())
-        go(ikg_packed_batch_kernel<SpecNextage, 2, true, true, P>);
-      else
-        go(ikg_packed_batch_kernel<SpecNextage, 0, true, true, P>);
-    };
-    if (a.rec_pool.cursor)
-      rec(std::true_type{});
+    if (need == 1 && capped_ok<1, true>())
+      go(ikg_packed_batch_kernel<SpecNextage, 1, true, true>);
+    else if (need == 2 && capped_ok<2, true>())
+      go(ikg_packed_batch_kernel<SpecNextage, 2, true, true>);
     else
-      rec(std::false_type{});
+      go(ikg_packed_batch_kernel<SpecNextage, 0, true, true>);
     if (a.rec_used) *a.rec_used = true;
     return hipGetLastError();
   }

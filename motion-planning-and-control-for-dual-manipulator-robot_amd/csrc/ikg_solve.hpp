@@ -41,19 +41,6 @@ __device__ inline void store_q(const KModel<T>* __restrict__ m, int arm, const T
 //   [16, ...): passive joints (passive_q order), padded to a multiple of 4
 constexpr int kRecRoot = 0, kRecArm0 = 1, kRecErr0 = 7, kRecPass = 8, kRecArm1 = 9, kRecErr1 = 15, kRecPassive = 16;
 constexpr int32_t kTrajEnded = 1 << 30;  // record count flag: the last is the iterate after max_iters
-constexpr int32_t kTrajNoRec = 1 << 29;  // record count flag: converged, but the record pool was full
-
-// Pooled records (batches whose (max_iters + 1) records per problem exceed the
-// record budget): a problem reserves max_iters + 1 - k0 records from a shared
-// pool when its errors first pass (k0), one atomic per problem; if the pool is
-// full it records nothing, ends there like the batch loop without records and
-// is flagged kTrajNoRec, and the continuation's trajectory kernel takes it
-// (ikg_collision.hip launch_collide_continue).
-struct RecPool {
-  unsigned long long* cursor = nullptr;  // records handed out so far (null: fixed slots per problem)
-  int32_t* base = nullptr;               // [B] each problem's first record in the pool (-1: none)
-  unsigned long long cap = 0;            // pool capacity, records
-};
 IKG_HD inline int rec_len(int n_passive) { return kRecPassive + ((n_passive + 3) & ~3); }
 
 template <typename T>
@@ -94,15 +81,14 @@ __device__ __forceinline__ void load_block8(const T* src, T (&v)[8]) {
 // iterate for the collision scan; that iterate's outputs are stored when reached.
 template <typename T>
 struct RecOut {
-  T* rec;               // this problem's records, (max_iters + 1) x rec_len (pooled: the pool)
-  int32_t* nrec;        // this problem's record count (| kTrajEnded, or kTrajNoRec)
+  T* rec;               // this problem's records, (max_iters + 1) x rec_len
+  int32_t* nrec;        // this problem's record count (| kTrajEnded)
   const T* qrow;        // its q0 row (passive joints)
   T* qo;                // its q_out row
   uint8_t* conv;        // its outputs at the first passing iterate
   int32_t* iters;
   T* err;
   int rl;               // rec_len
-  RecPool pool = {};    // pooled records (cursor non-null); pool.base points at this problem's slot
 };
 
 // Stop test of inverse_geometry.py:70 on squared norms (KParams::eps2):
@@ -119,10 +105,11 @@ __device__ inline bool both_below(T x, T xo, E eps2) {
 // float: this lane owns one arm (pair layout, partner = lane ^ 1); T = v2f:
 // this lane owns both arms (packed layout).  Returns (through refs) the final
 // q of this lane, the update count and the hand error norms at the returned q.
-// POOL (with REC): records reserved from the pool at the first passing
-// iterate; without it, this problem's fixed slot (no reservation state in the
-// loop: with it, the fixed-slot kernel ran 12% slower at C2, profiles/r05/collision/)
-template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false, bool POOL = false>
+// REC: every iterate from the first passing one on is recorded into this
+// problem's fixed slot (ikg_capi.hip sizes the launches so the slots fit the
+// record budget: no shared state, so a problem's records and answer do not
+// depend on which other problems share the launch or in what order they run)
+template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
 __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
                                   const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
                                   T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out,
@@ -130,7 +117,6 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   int k0 = -1;  // REC: the first iterate whose errors pass
   using E = typename LaneT<T>::E;
   E* recp = REC ? ro->rec : nullptr;  // this problem's records
-  bool norec = false;                 // REC, pooled: the pool was full at k0
   static_assert(!(DAMPED && is_packed<T>), "the packed layout implements lambda = 0 only");
   constexpr bool F1 = kFrame1<SP> && !DAMPED;  // frame-1 path, its own trig slots
   T sn[7], cs[7];
@@ -197,24 +183,7 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
       if (pass && k0 < 0) {  // the answer unless it collides: record 0, written out after the loop
         k0 = it;
         conv = true;
-        if constexpr (POOL) {  // reserve this problem's records in the pool
-          const unsigned long long need = (unsigned long long)(prm.max_iters + 1 - it);
-          unsigned long long b = 0;
-          if constexpr (is_packed<T>) {
-            b = atomicAdd(ro->pool.cursor, need);
-          } else {  // both lanes of the problem are here (the test reads both errors)
-            if (arm == 0) b = atomicAdd(ro->pool.cursor, need);
-            const unsigned lo = (unsigned)pair_swap_i32((int)(unsigned)b);
-            const unsigned hi = (unsigned)pair_swap_i32((int)(unsigned)(b >> 32));
-            if (arm != 0) b = ((unsigned long long)hi << 32) | lo;
-          }
-          norec = b + need > ro->pool.cap;
-          if (!norec) recp = ro->rec + (int64_t)b * ro->rl;
-          if (arm == 0) *ro->pool.base = norec ? -1 : (int32_t)b;
-        }
       }
-      if constexpr (POOL)
-        if (norec) break;  // no room: end at k0 as the loop without records would
       if (k0 >= 0) {
         if constexpr (is_packed<T>) {  // both arms' blocks from the one lane
           float b0[8], b1[8];
@@ -265,9 +234,7 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   if (any_of(ps == T(-12345.678))) it = -1;  // never true; keeps the padding live
 #endif
   if constexpr (REC) {
-    if (norec) {  // the caller writes the outputs at k0; the continuation's trajectory kernel takes it
-      if (arm == 0) *ro->nrec = kTrajNoRec;
-    } else if (k0 >= 0) {
+    if (k0 >= 0) {
       // the outputs at the first passing iterate, from its record (this lane's
       // own block of record 0): writing them inside the loop put a divergent
       // branch into every update (records-in-batch kernel 4% slower)
@@ -305,20 +272,20 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   nrm_out = sqrt(x);
   other_out = sqrt(xo);
   conv_out = conv;
-  return REC && k0 >= 0 && !norec;  // the outputs came from the records
+  return REC && k0 >= 0;  // the outputs came from the records
 }
 
 // Pair-layout batch kernel body (ikg_kernels.hip ikg_pair_batch_kernel, and the
 // model-specialised kernels ikg_jit.cpp compiles at run time with `m` pointing
 // at a constant copy of the model tables): one 64-lane wave per workgroup
 // holding `ppw` problems on lanes [0, 2 ppw).
-template <typename T, bool DAMPED, class SP, bool MED, bool REC = false, bool POOL = false>
+template <typename T, bool DAMPED, class SP, bool MED, bool REC = false>
 __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KParams<T>& prm,
                                        const T* __restrict__ targets, const T* __restrict__ q0, int64_t q0_stride,
                                        int64_t B, int64_t S, int ppw, T* __restrict__ q_out,
                                        uint8_t* __restrict__ conv_out, int32_t* __restrict__ iters_out,
                                        T* __restrict__ err_out, T* __restrict__ rec = nullptr,
-                                       int32_t* __restrict__ nrec = nullptr, RecPool pool = {}) {
+                                       int32_t* __restrict__ nrec = nullptr) {
   const int lane = threadIdx.x;
   const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
   const int arm = lane & 1;
@@ -336,15 +303,10 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
   T nrm, other;
   if constexpr (REC) {  // the continuation's records (ikg_collision.hip): outputs at the first passing iterate
     const int rl = rec_len(m->n_passive);
-    RecOut<T> ro{POOL ? rec : rec + p * (int64_t)(prm.max_iters + 1) * rl, nrec + p, qrow, q_out + p * m->nq,
+    RecOut<T> ro{rec + p * (int64_t)(prm.max_iters + 1) * rl, nrec + p, qrow, q_out + p * m->nq,
                  conv_out + p, iters_out + p, err_out + p * 2, rl};
-    if constexpr (POOL) {
-      ro.pool = pool;
-      ro.pool.base = pool.base + p;
-      if (arm == 0) pool.base[p] = -1;
-    }
     if (arm == 0) nrec[p] = 0;
-    if (solve_pair<T, DAMPED, SP, MED, true, POOL>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
+    if (solve_pair<T, DAMPED, SP, MED, true>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
     solve_pair<T, DAMPED, SP, MED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
   }

@@ -95,7 +95,7 @@ def _init_torch_runtime_first():
     links (/opt/rocm).  Both work in one process — torch tensors' device
     pointers go straight into our kernels — but only if torch's runtime
     initialises first: after ours, torch reports "No HIP GPUs are available"
-    (measured on the MI355X box, tools/probe/order.py).  So when torch is
+    (measured on the MI355X box by importing the library before and after torch).  So when torch is
     importable, let it claim the device before the library loads."""
     try:
         import torch

@@ -185,6 +185,89 @@ def test_c2_full_collision_fp64(threads):
     assert rep["q_over_1e9"] == 0 and rep["err_max_abs_diff_success"] <= 1e-9
 
 
+def _scaled_scene(sc, delta):
+    """The collision scene with every geometry dimension moved by delta (m)."""
+    out = dict(sc)
+    out["geoms"] = [dict(g) for g in sc["geoms"]]
+    for g in out["geoms"]:
+        d = np.asarray(g["dims"], dtype=np.float64)
+        g["dims"] = np.maximum(d + delta * (d > 0), 0.0)
+    return out
+
+
+def _collision_margin(sc, q, target):
+    """The smallest inflation/deflation (m) of every geometry that changes
+    collision(q) (tools.py:25-35), or None when none up to 1e-3 does."""
+    for d in (1e-7, 1e-6, 1e-5, 1e-4, 1e-3):
+        a = c_oracle.collision(_scaled_scene(sc, d), q[None], target[None])[0]
+        b = c_oracle.collision(_scaled_scene(sc, -d), q[None], target[None])[0]
+        if a != b:
+            return d
+    return None
+
+
+def test_c3_full_collision_fp32(threads):
+    """C3's 65,536 fp32 targets WITH the collision term
+    (bench.py --collision --dtype f32 --batch 65536: the packed layout's records,
+    the fused first check and records scan) against the fp64 C restatement with
+    the collision term (oracle/ikg_oracle.c, inverse_geometry.py:56-100 with
+    tools.py:25-35).  Gates: end-effector SE(3) error <= 1e-4 on every problem
+    both call successful; update counts within +-2 there; and every problem
+    whose success flag or count differs beyond that is listed with the two
+    margins that can decide it at the earlier of the two stops k: the fp64
+    loop's stop-test margin after k updates (|e| / eps - 1) and the smallest
+    geometry inflation that changes collision(q_k) -- each must be a knife
+    edge that fp32 rounding can tip (stop margin < 1e-3 relative, or the
+    collision decision changed by moving the surfaces <= 1e-4 m)."""
+    from ikgrasp.collision import load_nextage_scene
+    from ikgrasp.solver import IKSolver
+    from ikgrasp.workload import uniform_targets
+    from oracle import collision_oracle
+    scene = load_nextage_scene()
+    B = 65536
+    tg = uniform_targets(B, seed=0)
+    s = IKSolver(device=0, scene=scene)
+    try:
+        g = s.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
+        sc = collision_oracle.prepare(json.loads(scene.to_json()))
+        q, ok, it, err = c_oracle.solve_collision(sc, tg, np.zeros(15), threads=threads)
+        gc, git = g.converged.astype(bool), g.iters.astype(int)
+        both = ok & gc
+        it_off = np.abs(git - it)
+        ee = _ee_err(s, q[both], g.q[both])
+        odd = np.nonzero((ok != gc) | (both & (it_off > 2)))[0]
+        rows = []
+        for i in odd:
+            k = int(min(git[i], it[i]))
+            # the fp64 iterate after exactly k updates (eps = 0: the stop test never passes)
+            qk, _, _, ek = c_oracle.solve_ex(tg[i][None], np.zeros(15), 0, max_iters=k, eps=0.0, threads=1)
+            col = bool(c_oracle.collision(sc, qk, tg[i][None])[0])
+            rows.append(dict(index=int(i), fp32=[bool(gc[i]), int(git[i])], fp64=[bool(ok[i]), int(it[i])],
+                             earlier_stop=k, fp64_err_at_k=[float(ek[0][0]), float(ek[0][1])],
+                             stop_margin_rel=float(max(ek[0]) / EPS - 1.0), fp64_collides_at_k=col,
+                             collision_margin_m=_collision_margin(sc, qk[0], tg[i])))
+        ok_rows = [r for r in rows if abs(r["stop_margin_rel"]) < 1e-3 or
+                   (r["collision_margin_m"] is not None and r["collision_margin_m"] <= 1e-4)]
+        unexplained = [r for r in rows if r not in ok_rows]
+        rep = dict(config="C3 + collision term", B=B, dtype="f32 kernel vs fp64 oracle with the collision term",
+                   oracle="C restatement with the collision term (oracle/ikg_oracle.c ikg_oracle_solve_collision)",
+                   oracle_success=int(ok.sum()), gpu_success=int(gc.sum()),
+                   success_flips=int((ok != gc).sum()), iters_outside_pm2=int((both & (it_off > 2)).sum()),
+                   iters_max_abs_diff_success=int(it_off[both].max()) if both.any() else 0,
+                   iters_hist_success={str(k): int((it_off[both] == k).sum()) for k in range(3)},
+                   ee_err_max=float(ee.max()) if len(ee) else 0.0,
+                   ee_err_p99=float(np.quantile(ee, 0.99)) if len(ee) else 0.0, ee_tolerance=EE_TOL,
+                   listed=rows, unexplained=unexplained)
+        helpers.report("c3_collision_vs_oracle", rep)
+        print(f"C3 + collision fp32: {rep['success_flips']} success flips, {rep['iters_outside_pm2']} counts "
+              f"outside +-2, ee max {rep['ee_err_max']:.3g}, {len(unexplained)} unexplained")
+        assert rep["ee_err_max"] <= EE_TOL
+        assert not unexplained, unexplained
+        assert len(rows) <= B // 1000
+    finally:
+        s.close()
+
+
 def test_c3_full_fp32(solver, threads):
     from ikgrasp.workload import uniform_targets
     B = 65536
