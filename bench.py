@@ -224,7 +224,21 @@ def multistart_bytes(dtype, T, S, nq=15):
     return T * per_target + S * nq * s + T * S * per_problem
 
 
-SHADER_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md); the latency model's cycles -> ms
+SHADER_GHZ = 2.4  # MI355X peak engine clock (MI355X_MICROARCH.md): used only without a measured clock
+
+
+def measured_clock(kernel, dtype):
+    """The in-kernel shader clock the stage-stamp build measured on this
+    kernel (tools/stage_clock.py: Δs_memtime / Δs_memrealtime x 100 MHz over
+    every wave's loop, after >= 2 s of back-to-back launches) -> (GHz, source)."""
+    p = os.path.join(ROOT, "profiles", f"stage_{kernel}_{dtype}.json")
+    if os.path.exists(p):
+        with open(p) as f:
+            d = json.load(f)
+        ghz = (d.get("c2") or d.get("forced") or {}).get("clock_GHz")
+        if ghz:
+            return ghz, os.path.relpath(p, ROOT), d
+    return SHADER_GHZ, "assumed peak engine clock (MI355X_MICROARCH.md)", None
 
 
 def latency_block(kernel, dtype, med, kern_ms, max_iters, waves, simds):
@@ -240,8 +254,9 @@ def latency_block(kernel, dtype, med, kern_ms, max_iters, waves, simds):
         return None
     with open(p) as f:
         m = json.load(f)
-    pred = max_iters * m["in_order_cycles"] / (SHADER_GHZ * 1e6)
-    return {
+    ghz, clk_src, stage = measured_clock(kernel, dtype)
+    pred = max_iters * m["in_order_cycles"] / (ghz * 1e6)
+    out = {
         "bound": "per-wave in-order issue of one update's dependent instruction stream (waves <= SIMDs)",
         "updates_longest_wave": max_iters,
         "instructions_per_update": m["instructions_per_update"], "valu_per_update": m["valu_per_update"],
@@ -249,10 +264,18 @@ def latency_block(kernel, dtype, med, kern_ms, max_iters, waves, simds):
         "critical_path_cycles_per_update": m["critical_path_cycles"],
         "model_cycles_per_update": m["in_order_cycles"], "stall_cycles_per_update": m["stall_cycles"],
         "register_copies_per_update": m.get("register_copies_per_update"),
-        "clock_GHz": SHADER_GHZ, "predicted_ms": pred, "measured_ms": kern_ms,
-        "measured_cycles_per_update": kern_ms * SHADER_GHZ * 1e6 / max_iters,
+        "clock_GHz": ghz, "clock_source": clk_src, "predicted_ms": pred, "measured_ms": kern_ms,
+        "measured_cycles_per_update": kern_ms * ghz * 1e6 / max_iters,
         "frac": pred / kern_ms, "source": os.path.relpath(p, ROOT),
     }
+    if stage and stage.get("forced"):
+        f = stage["forced"]
+        out["stages_measured"] = {
+            "cycles_per_update_each_stage_alone": f["diag_stage_cycles_per_update"],
+            "stamped_loop_cycles_per_update": f["diag_loop_cycles_per_update"],
+            "is": "s_memtime stamps between the stages (diagnostic build, every lane runs 1,000 updates); "
+                  "fenced stages cannot overlap, so they sum above the product loop's cycles"}
+    return out
 
 
 def roofline(dtype, kernel, med, kern_ms, sum_iters, waves, simds, abytes, traffic, traffic_src, max_iters=None):
@@ -306,7 +329,7 @@ def iters_hist(iters, max_iters=1000, width=50):
     return h
 
 
-REC_BUDGET_MB = 6144  # ikg_capi.hip kRecBudgetMB (IKG_REC_BUDGET_MB overrides)
+REC_BUDGET_MB = 24576  # ikg_capi.hip kRecBudgetMB (IKG_REC_BUDGET_MB overrides)
 
 
 def collision_kernels(kname, dtype, B, S=0):

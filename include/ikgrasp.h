@@ -36,7 +36,7 @@
  *     collision term, a problem that converges into collision runs on in the
  *     batch kernel itself, which records every later iterate into the
  *     problem's own fixed slot; a batch whose records exceed the record
- *     budget (IKG_REC_BUDGET_MB, 6 GiB) is solved as several launches of
+ *     budget (IKG_REC_BUDGET_MB, 24 GiB) is solved as several launches of
  *     equal size whose records fit, every launch in the layout the whole
  *     batch would take, so the answer is the one-launch answer.  (Models the
  *     batch kernel does not record for -- generic or run-time-compiled
@@ -71,10 +71,11 @@
  * Scratch memory
  *   - Uncaptured solves take their scratch from a stream-ordered pool the
  *     model owns (one per device it solves on).  The pool keeps up to
- *     6.5 GiB of freed memory reserved for the next solve (the collision
- *     records are the large item, up to 6 GiB per solve; environment
+ *     1.25 GiB of freed memory reserved for the next solve (environment
  *     IKG_WS_KEEP_MB overrides the amount) and releases the rest at the next
- *     synchronisation.  ikg_model_trim synchronises each such device and
+ *     synchronisation.  The collision records are the large item: up to the
+ *     record budget (24 GiB) while a collision solve runs, released after it
+ *     beyond what the pool keeps.  ikg_model_trim synchronises each such device and
  *     releases everything the pools hold unused; ikg_model_destroy
  *     synchronises and destroys the pools.  Released memory goes back to the
  *     HIP runtime, which keeps it mapped for later pools and allocations of

@@ -232,18 +232,23 @@ static bool rec_in_batch() {
   const char* e = getenv("IKG_TRAJ_REC");
   return !(e && atoi(e) == 0);
 }
-// Budget 6 GiB, ~2% of an MI355X's 288 GB (C2 fp64: 656 MB; C3 fp32: 5.2
-// GB): the records of one launch, (max_iters + 1) per problem in fixed slots.
-// A batch whose records exceed it is solved in chunks of equal size that fit
-// (C4's 131,072-problem fp64 share: 4 chunks; C5's 131,072 fp32 problems: 2),
-// one launch sequence per chunk on the stream.  Fixed slots carry no shared
-// state, so a problem's answer does not depend on the chunking or on the order
-// its launch's waves run in.  (Round 5 handed out records from one pool by a
-// per-problem atomic instead; when it ran dry, which problems fell back to the
-// record-free continuation depended on wave scheduling, and that path agrees
-// with the records only to rounding -- VERDICT r5)
-// IKG_REC_BUDGET_MB overrides.
-constexpr size_t kRecBudgetMB = 6144;
+// Budget 24 GiB (~8% of an MI355X's 288 GB, held only while a collision solve
+// runs: the model's scratch pool keeps 1.25 GiB between solves, ikg_launch.hpp
+// ws_keep_bytes): the records of one launch, (max_iters + 1) per problem in
+// fixed slots (C2 fp64: 656 MB; C3 fp32: 5.2 GB; C5's 131,072 fp32 problems:
+// 10.5 GB; C4's 131,072-problem fp64 share: 21 GB).  A batch whose records
+// exceed it is solved in chunks of equal size that fit (C4 on one GPU, fp64:
+// 7 chunks), one launch sequence per chunk on the stream.  Fixed slots carry
+// no shared state, so a problem's answer does not depend on the chunking or on
+// the order its launch's waves run in.  (Round 5 handed out records from one
+// pool by a per-problem atomic instead; when it ran dry, which problems fell
+// back to the record-free continuation depended on wave scheduling, and that
+// path agrees with the records only to rounding -- VERDICT r5)
+// Measured against round 5's pool (profiles/r06/records/): C2 and C3 + collision
+// unchanged; C4 share fp64 + collision 6.44 ms pooled, 6.43 in one launch at
+// 24 GiB, 6.67 in two at 12 GiB, 10.0 in four at 6 GiB; C5 + collision 3.58 ms
+// pooled, 3.72 in fixed slots.  IKG_REC_BUDGET_MB overrides.
+constexpr size_t kRecBudgetMB = 24576;
 static size_t rec_budget() {
   if (const char* e = getenv("IKG_REC_BUDGET_MB")) return (size_t)atoll(e) << 20;
   return kRecBudgetMB << 20;

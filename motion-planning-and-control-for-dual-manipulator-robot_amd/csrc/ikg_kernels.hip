@@ -42,8 +42,13 @@ namespace ikg {
 // step's LQ branch (pinv_step_f1) is cold, so spilling around it keeps the
 // loop at the occupancy it had without it (fp64 226 VGPRs: 2 waves; fp32
 // 103: 4); without the bound its registers took fp64 to 1 wave per SIMD.
+// IKG_PAIR_MINW64: the fp64 bound as a build knob (a
+// 3-wave build, at most 168 VGPRs, A/B'd in the throughput regime)
+#ifndef IKG_PAIR_MINW64
+#define IKG_PAIR_MINW64 2
+#endif
 template <typename T, bool DAMPED, class SP>
-constexpr int kPairMinWaves = (kFrame1<SP> && !DAMPED) ? (sizeof(T) == 8 ? 2 : 4) : 1;
+constexpr int kPairMinWaves = (kFrame1<SP> && !DAMPED) ? (sizeof(T) == 8 ? IKG_PAIR_MINW64 : 4) : 1;
 
 template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
 __global__ __launch_bounds__(64)
@@ -67,6 +72,19 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                            err_out, rec, rec_n);
 }
 
+
+#ifdef IKG_STAGE_CLOCK
+// the stage stamps of the pair kernel's loop (ikg_solve.hpp g_stage, this
+// translation unit's copy); tools/stage_clock.py
+extern "C" int ikg_debug_stage(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stage), sizeof(g_stage)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stage), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 #ifdef IKG_SING_COUNT
 extern "C" int ikg_debug_sing(unsigned long long* out, int reset) {

@@ -111,15 +111,18 @@ inline void* ws_take_pending(WsState& st, int dev, size_t bytes, size_t* got) {
 }
 
 // How much freed scratch a model's pool keeps mapped across synchronisations
-// (its release threshold): 6.5 GiB by default -- the collision records
-// budget (6 GiB, ikg_capi.hip rec_budget) plus the continuation's workspaces,
-// so a solve that repeats finds its scratch in the pool -- and anything above
-// that goes back to the driver at the next synchronisation.
+// (its release threshold): 1.25 GiB by default -- a C2 collision solve's
+// records (656 MB) and every record-free solve's scratch stay mapped for the
+// next solve; anything above goes back to the driver at the next
+// synchronisation, so an idle model holds at most 1.25 GiB per device.  A
+// larger collision solve maps its records afresh each time: C3 fp32 + collision
+// (5.2 GB) 1.82 -> 1.93 ms, the C4 share and C5 + collision within their spread
+// (profiles/r06/records/; round 5 kept 6.5 GiB).
 // IKG_WS_KEEP_MB overrides (0 = keep nothing, as the device's default pool).
 inline uint64_t ws_keep_bytes() {
   static const uint64_t v = [] {
     const char* e = getenv("IKG_WS_KEEP_MB");
-    return e ? (uint64_t)strtoull(e, nullptr, 10) << 20 : (uint64_t)6656 << 20;
+    return e ? (uint64_t)strtoull(e, nullptr, 10) << 20 : (uint64_t)1280 << 20;
   }();
   return v;
 }

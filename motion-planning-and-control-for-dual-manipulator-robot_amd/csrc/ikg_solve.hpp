@@ -91,6 +91,33 @@ struct RecOut {
   int rl;               // rec_len
 };
 
+// Diagnostic build only (-DIKG_STAGE_CLOCK, tools/stage_clock.py; no stamp
+// exists in the product kernels): shader-clock stamps (s_memtime) between the
+// stages of every update of the frame-1 loop, and s_memrealtime (100 MHz) around
+// the loop, per wave, summed into g_stage by lane 0 of every wave:
+//   [0] waves  [1] updates  [2] loop memtime  [3] loop memrealtime
+//   [4] FK + log6 (arm_fk_error_f1)  [5] solve (pinv_step_f1)
+//   [6] exchange + stop test  [7] integrate + clamp (arm_update)
+//   [8] trig advance (trig_advance_f1)
+// Each stamp is one asm statement with its lgkmcnt wait, fenced by scheduling
+// barriers so no stage's instructions move across it (MI355X_MICROARCH.md
+// DVFS item 6, cdna_hip_programming.md "In-kernel stamps").
+#ifdef IKG_STAGE_CLOCK
+static __device__ unsigned long long g_stage[16];
+#define IKG_STAMP(t)                                                                          \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");                 \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+  } while (0)
+#define IKG_RSTAMP(t)                                                                         \
+  do {                                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                        \
+  } while (0)
+#endif
+
 // Stop test of inverse_geometry.py:70 on squared norms (KParams::eps2):
 // pair layout = this lane's hand and the partner's; packed = both halves.
 template <typename T, typename E>
@@ -141,6 +168,11 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 #pragma unroll
   for (int i = 0; i < 8; ++i) pad[i] = qc + T(i);
 #endif
+#ifdef IKG_STAGE_CLOCK
+  unsigned long long sc_acc[5] = {0, 0, 0, 0, 0}, sc_t0 = 0, sc_t1 = 0, sc_r0, sc_r1, sc_l0, sc_l1;
+  IKG_RSTAMP(sc_r0);
+  IKG_STAMP(sc_l0);
+#endif
   for (;;) {
 #ifdef IKG_PAD_OPS
 #pragma unroll
@@ -161,8 +193,18 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     T dq[6], alpha, beta, s;
     if constexpr (F1) {
       ArmStateF1<T> st;
+#ifdef IKG_STAGE_CLOCK
+      IKG_STAMP(sc_t0);
+      x = arm_fk_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, tkp, resync);
+      IKG_STAMP(sc_t1);
+      sc_acc[0] += sc_t1 - sc_t0;
+      pinv_step_f1<T, SP, PairX, !REC>(m, arm, st, sn, cs, dq, s);
+      IKG_STAMP(sc_t0);
+      sc_acc[1] += sc_t0 - sc_t1;
+#else
       x = arm_fk_error_f1<T, SP>(m, arm, sn, cs, RT, tT, st, tkp, resync);
       pinv_step_f1<T, SP, PairX, !REC>(m, arm, st, sn, cs, dq, s);
+#endif
     } else {
     ArmState<T> st;
     x = arm_fk_error<T, SP>(m, arm, sn, cs, RT, tT, st, nullptr, tkp, resync);
@@ -220,13 +262,37 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     q_old[0] = qc;
 #pragma unroll
     for (int k = 0; k < kArmDof; ++k) q_old[k + 1] = qa[k];
+#ifdef IKG_STAGE_CLOCK
+    IKG_STAMP(sc_t1);
+    sc_acc[2] += sc_t1 - sc_t0;
+#endif
     arm_update(m, arm, T(prm.dt), s, dq, qc, qa, limp);
     ++it;
-    if constexpr (F1)
+#ifdef IKG_STAGE_CLOCK
+    IKG_STAMP(sc_t0);
+    sc_acc[3] += sc_t0 - sc_t1;
+#endif
+    if constexpr (F1) {
       trig_advance_f1<T, MED>(m, arm, qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
-    else
+#ifdef IKG_STAGE_CLOCK
+      IKG_STAMP(sc_t1);
+      sc_acc[4] += sc_t1 - sc_t0;
+#endif
+    } else
       trig_advance<T, MED ? 1 : IKG_GENERIC_MED>(qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
   }
+#ifdef IKG_STAGE_CLOCK
+  IKG_STAMP(sc_l1);
+  IKG_RSTAMP(sc_r1);
+  if (threadIdx.x == 0) {  // lane 0 of the wave: its problem's loop ran longest only in forced runs (every lane to max_iters)
+    atomicAdd(&g_stage[0], 1ull);
+    atomicAdd(&g_stage[1], (unsigned long long)it);
+    atomicAdd(&g_stage[2], sc_l1 - sc_l0);
+    atomicAdd(&g_stage[3], sc_r1 - sc_r0);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) atomicAdd(&g_stage[4 + k], sc_acc[k]);
+  }
+#endif
 #ifdef IKG_PAD_OPS
   T ps = T(0);
 #pragma unroll

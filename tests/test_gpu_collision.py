@@ -393,7 +393,7 @@ def test_record_chunks_give_the_one_launch_answer(csolver, dtype, monkeypatch):
     the budget runs in chunks whose fixed record slots fit it (ikg_capi.hip
     rec_chunk), never from a shared pool, so a problem's answer does not depend
     on the chunking or on wave order.  C2's 4,096 targets: one launch (the
-    default 6 GiB budget), and a 4 MB budget (fp64: 25 problems per launch,
+    default 24 GiB budget), and a 4 MB budget (fp64: 25 problems per launch,
     fp32: 52) solved twice -- bit for bit equal.  Both first-check schedules
     (IKG_PRESCAN=1: the check fused into the records scan, the default up to
     65,536 problems per launch; 0: pre-screen + compaction + scan, the default

@@ -4,7 +4,7 @@
 #   ABTAG=<dir under gpurun_out>  CONFIGS="c2_f64 c2_f64_forced c3_f32 rand_f64 c2col_f64 c4s_f64"
 #   ABTESTS=1: then the GPU tests on the in-tree library
 ROOT=$(pwd); O=$ROOT/gpurun_out/${ABTAG:-ab}; mkdir -p $O
-L="$ROOT/ab_libs/*.so"
+L=${ABLIBS:-"$ROOT/ab_libs/*.so"}  # ABLIBS: space-separated library paths or globs
 run() {  # name rounds batch dtype [env...]
   n=$1 r=$2 b=$3 d=$4; shift 4
   env ABL_ROUNDS=$r "$@" timeout -k 10 300 python tools/ablate.py $b $d "$L" > $O/$n.txt 2>&1 || exit 3

@@ -23,7 +23,7 @@ declare -A ARGS=(
 for rep in $(seq 1 ${REPS:-3}); do
   for cfg in $CONFIGS; do
     for v in $VARIANTS; do
-      f=$O/${cfg}__${v//[=,]/_}__$rep.json
+      f=$O/${cfg}__${v//[=,\/]/_}__$rep.json
       env $( [ "$v" = base ] || echo $v | tr ',' ' ') timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra ${ARGS[$cfg]} > $f 2>> $O/bench.err
       rc=$?; [ $rc -eq 0 ] || { echo "FATAL $cfg $v rc=$rc"; exit $rc; }
     done
@@ -33,7 +33,8 @@ python - <<PY | tee $O/summary.txt
 import json, glob, os, collections
 rows = collections.defaultdict(list)
 for f in sorted(glob.glob("$O/*.json")):
-    cfg, v, rep = os.path.basename(f)[:-5].split("__")
+    parts = os.path.basename(f)[:-5].split("__")
+    cfg, v, rep = parts[0], "__".join(parts[1:-1]), parts[-1]
     d = json.load(open(f))
     rows[(cfg, v)].append((d["ms_per_step"], d["roofline"]["kernel_ms"]))
 for (cfg, v), r in sorted(rows.items()):

@@ -5,7 +5,9 @@ usage: pmc_probe.py B dtype ppw reps [--save-iters path.npy] [--collision]
 --yaw: cube yaw ~ U[-RAD, RAD] (bench.py extra.c2_yaw); --seed: the targets'
 seed (bench.py c4_strong: 7); --randq0: a random seed row per problem
 (workload.random_seeds, seed 1000 -- the multi-start's per-seed problems:
-the pair kernel's medium-range instantiation); --variant: ikg_variant."""
+the pair kernel's medium-range instantiation); --variant: ikg_variant;
+--multistart S: B targets x S seeds (bench.py --multistart: random_seeds
+seed 1000, seed row 0 = q0 = 0), the whole multi-start launch."""
 import os
 import sys
 
@@ -38,8 +40,19 @@ cv = torch.empty(B, dtype=torch.uint8, device=dev)
 it = torch.empty(B, dtype=torch.int32, device=dev)
 er = torch.empty((B, 2), dtype=tdt, device=dev)
 st = torch.cuda.current_stream().cuda_stream
+MS = opt("--multistart", 0, int)
+if MS:
+    from ikgrasp.workload import random_seeds  # noqa: E402
+    sd = random_seeds(s.model, MS, seed=1000)
+    sd[0] = 0.0
+    seeds = torch.tensor(sd, dtype=tdt, device=dev)
+    best = torch.empty(B, dtype=torch.int32, device=dev)
 for _ in range(reps):
-    s.solve_into(tg, q0, qo, cv, it, er, code, st, ppw=ppw, check_collision=col, variant=opt("--variant", 0, int))
+    if MS:
+        s.solve_multistart_into(tg, seeds, qo, cv, it, er, best, code, st, check_collision=col,
+                                variant=opt("--variant", 0, int))
+    else:
+        s.solve_into(tg, q0, qo, cv, it, er, code, st, ppw=ppw, check_collision=col, variant=opt("--variant", 0, int))
 torch.cuda.synchronize()
 print("sum iters", int(it.to(torch.int64).sum()), "converged", int(cv.sum()))
 if "--save-iters" in sys.argv:

@@ -34,15 +34,23 @@ def per_solve(d, counter, solves):
     return tot / solves
 
 
-def main_collision(pmc_dir, dtype, B, tag, solves):
-    fetch = per_solve(os.path.join(pmc_dir, f"fetch_b{B}_{dtype}_col"), "FETCH_SIZE", solves)
-    write = per_solve(os.path.join(pmc_dir, f"write_b{B}_{dtype}_col"), "WRITE_SIZE", solves)
-    out = {"kernel": "collision solve: every ikg_* kernel of one ikg_solve_batch with check_collision",
+def main_collision(pmc_dir, dtype, B, tag, solves, S=0, col=True):
+    # every ikg_* dispatch of a run over its solves: a collision solve, or
+    # (S > 0) a multi-start launch with or without the collision term
+    x = (f"_s{S}" if S else "") + ("_col" if col else "")
+    fetch = per_solve(os.path.join(pmc_dir, f"fetch_b{B}_{dtype}{x}"), "FETCH_SIZE", solves)
+    write = per_solve(os.path.join(pmc_dir, f"write_b{B}_{dtype}{x}"), "WRITE_SIZE", solves)
+    what = (f"multi-start launch ({S} seeds x {B} targets): every ikg_* kernel of one ikg_solve_multistart"
+            if S else "collision solve: every ikg_* kernel of one ikg_solve_batch") + \
+        (" with check_collision" if col else "")
+    out = {"kernel": what,
            "dtype": dtype, "batch": B, "round": tag, "solves": solves,
            "FETCH_SIZE_KiB": fetch, "WRITE_SIZE_KiB": write, "hbm_bytes_per_launch": (2 * fetch + write) * 1024,
            "note": "2 x FETCH_SIZE (gfx950 wide-read correction) + WRITE_SIZE, KiB -> bytes; all dispatches of "
                    "the run over the number of identical solves"}
-    path = os.path.join(ROOT, "profiles", f"pmc_{dtype}_b{B}_col.json")
+    if S:
+        out["seeds_per_target"] = S
+    path = os.path.join(ROOT, "profiles", f"pmc_{dtype}_b{B}{x}.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     print(path, out)
@@ -68,6 +76,12 @@ def main(pmc_dir, dtype, B, tag, sfx=""):
 
 
 if __name__ == "__main__":
+    # pmc_summary.py DIR dtype B tag --multistart S SOLVES [--collision]
+    if "--multistart" in sys.argv:
+        i = sys.argv.index("--multistart")
+        main_collision(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[i + 2]),
+                       S=int(sys.argv[i + 1]), col="--collision" in sys.argv)
+        sys.exit(0)
     if "--collision" in sys.argv:
         main_collision(sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4], int(sys.argv[6]))
         sys.exit(0)
