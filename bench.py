@@ -334,20 +334,20 @@ REC_BUDGET_MB = 24576  # ikg_capi.hip kRecBudgetMB (IKG_REC_BUDGET_MB overrides)
 
 def collision_kernels(kname, dtype, B, S=0):
     """The kernels a collision solve runs, by the C-ABI's rules
-    (ikg_capi.hip rec_chunk, ikg_collision.hip prescan_on): the batch kernel
-    with records in launches whose fixed record slots fit the budget, then per
-    launch either the first check fused into the records scan (up to 65,536
-    problems per launch, IKG_PRESCAN) or pre-screen + compaction + scan."""
-    slot = (8 if dtype == "f64" else 4) * 20 * 1001 * max(S, 1)  # one unit's records (a target's S seeds)
+    (ikg_capi.hip rec_chunk, ikg_collision.hip launch_collide_continue): the
+    batch kernel writing window checkpoints, in launches whose fixed slots fit
+    the budget, then per launch the first check with the window-box tests
+    (ikg_traj_scan_kernel round -2), the compaction, the resume launch of the
+    batch kernel (windows left to regenerate) and the records scan."""
+    esz = 8 if dtype == "f64" else 4
+    slot = esz * (20 * 1001 + 64 * 33) * max(S, 1)  # one unit's records + checkpoints (a target's S seeds)
     budget = int(os.environ.get("IKG_REC_BUDGET_MB", str(REC_BUDGET_MB))) << 20
     cap = max(1, budget // slot)
     chunks = 1 if B <= cap else -(-B // cap)
     per = -(-B // chunks) * max(S, 1)  # problems per launch
-    pre = os.environ.get("IKG_PRESCAN")
-    fused = (int(pre) != 0) if pre is not None else per <= 65536
-    label = kname + " (records every iterate past the first passing one) + " + (
-        "ikg_traj_scan_kernel (first check fused with the records scan)" if fused else
-        "ikg_prescreen_kernel + ikg_compact_count_kernel + ikg_compact_write_kernel + ikg_traj_scan_kernel")
+    label = (kname + " (window checkpoints past the first passing iterate) + ikg_traj_scan_kernel (first check"
+             " and window boxes) + ikg_compact_count_kernel + ikg_compact_write_kernel + " + kname +
+             " (resume: windows left) + ikg_traj_scan_kernel (records scan)")
     if chunks > 1:
         label += f"; {chunks} launch sequences of {per} problems (records budget {budget >> 20} MB)"
     return label, "the whole solve (all its kernels)"

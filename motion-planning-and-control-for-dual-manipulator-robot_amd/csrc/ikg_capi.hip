@@ -254,11 +254,16 @@ static size_t rec_budget() {
   return kRecBudgetMB << 20;
 }
 
-// bytes of one problem's record slot
+// bytes of one problem's record slot (the regenerated records) and window
+// checkpoints (ikg_solve.hpp kWin)
 template <typename T>
-static size_t rec_slot_bytes(const ikg_params& params, int nq) {
+static size_t rec_records_bytes(const ikg_params& params, int nq) {
   const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
   return sizeof(T) * rl * ((size_t)params.max_iters + 1);
+}
+template <typename T>
+static size_t rec_slot_bytes(const ikg_params& params, int nq) {
+  return rec_records_bytes<T>(params, nq) + sizeof(T) * (size_t)ikg::ck_per_problem(params.max_iters);
 }
 
 // units (problems, or multi-start targets of `per_unit` problems each) per
@@ -279,17 +284,19 @@ static int64_t rec_chunk(const ikg_params& params, int nq, int64_t units, int64_
 template <typename T>
 void* offer_records(ikg_model* model, ikg::BatchArgs& a, const ikg_params& params, int64_t n, int nq, hipStream_t s,
                     bool* rec_used) {
-  const size_t b_rec = (rec_slot_bytes<T>(params, nq) * (size_t)n + 255) & ~(size_t)255;
+  const size_t b_rec = (rec_records_bytes<T>(params, nq) * (size_t)n + 255) & ~(size_t)255;
+  const size_t b_ck = (sizeof(T) * (size_t)ikg::ck_per_problem(params.max_iters) * (size_t)n + 255) & ~(size_t)255;
   const size_t b_n = (sizeof(int32_t) * (size_t)n + 255) & ~(size_t)255;
   void* rec = nullptr;
-  if (ikg::ws_alloc(&model->ws, &rec, b_rec + b_n, s) != hipSuccess) {
+  if (ikg::ws_alloc(&model->ws, &rec, b_rec + b_ck + b_n, s) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
   a.rec = rec;
-  a.rec_n = (int32_t*)((char*)rec + b_rec);
-  ikg::ws_trace("alloc rec", rec, b_rec + b_n, s);
-  ikg::poison_float(rec, b_rec, s);
+  a.ck = (char*)rec + b_rec;
+  a.rec_n = (int32_t*)((char*)rec + b_rec + b_ck);
+  ikg::ws_trace("alloc rec", rec, b_rec + b_ck + b_n, s);
+  ikg::poison_float(rec, b_rec + b_ck, s);
   ikg::poison_int(a.rec_n, sizeof(int32_t) * (size_t)n, s);
   a.rec_used = rec_used;
   return rec;
@@ -459,6 +466,7 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
     rec = offer_records<T>(model, tmp, *params, a.rec_chunk * S, nq, s, &rec_used);
     a.rec = tmp.rec;
     a.rec_n = tmp.rec_n;
+    a.ck = tmp.ck;
     a.rec_used = tmp.rec_used;
     if (!rec) a.rec_chunk = 0;
   }

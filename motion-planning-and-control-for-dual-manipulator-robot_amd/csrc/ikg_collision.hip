@@ -1392,10 +1392,15 @@ struct TrajWs {
   int64_t slots;      // slots per parity
   int by_p = 0;       // records, counts and it0 indexed by problem (the pair kernel's records)
   int cert = 1;       // inscribed-ball certificates before the witness tests (IKG_SCAN_CERT=0: off)
-  // round -2 (records, no separate pre-screen): problem i = index i of the
-  // batch, every converged one checked first; wit_out[i] = the colliding pair
-  // found, -1 if none or not converged
+  // round -2 (window checkpoints, ikg_solve.hpp kWin): problem i = index i of
+  // the batch, every converged one checked first, then a colliding one's
+  // windows tested against certificates; wit_out[i] = the colliding pair
+  // found when some window is left to regenerate (flagged in wmask), -1 if
+  // none, not converged or answered
   int32_t* wit_out = nullptr;
+  const T* ck = nullptr;        // the batch kernel's window checkpoints
+  uint32_t* wmask = nullptr;    // per problem, the windows left (mask_words each): written by round -2, read by round 0
+  int box = 1;                  // round -2: window boxes tested (IKG_BOX_COVER)
 };
 
 // IKG_SCAN_CERT=0: the records scan without inscribed-ball certificates (A/B
@@ -1411,16 +1416,23 @@ static int scan_cert() {
 // wave per SIMD, ~8.5 windows each at C3) took C3 + collision 2.21 ms against
 // 1.98 (profiles/r05/collision/scan_waves/); IKG_SCAN_WAVES (read at every
 // launch) sets it for A/Bs
-// With records, the first check and the records scan of a problem in one wave
-// of one launch (traj_scan_body round -2) instead of the pre-screen, the
-// compaction and a scan over the listed problems: C2 + collision 1.212 ->
-// 1.199 ms, C3 + collision 1.807 -> 1.800, but C5 + collision (131,072
-// problems per launch) 3.502 -> 3.574 (profiles/r05/collision/prescan/), so
-// up to 65,536 problems per launch.  IKG_PRESCAN=0/1 (read at every launch)
-// forces either form.
-static bool prescan_on(int64_t B) {
+// IKG_BOX_COVER=0 (read at every launch): round -2 proves no window by its box,
+// so every problem that collides at its first passing iterate has all its
+// records regenerated and scanned -- the round-5 records' work, for the tests
+// that pin the window form's answers to it (and for A/Bs)
+// The first check of a records solve (ikg_first_check_kernel): fused with the
+// window boxes over the whole batch up to 65,536 problems per launch; above,
+// the lean pre-screen kernel checks every converged problem and the boxes run
+// over its colliding list (the fused kernel's registers -- certificate code --
+// hold it to 1 wave per SIMD in fp64: 1.6 ms for C4's 131,072-problem share).
+// IKG_PRESCAN=1/0 (read at every launch) forces the fused / split form.
+static bool first_fused(int64_t B) {
   const char* e = getenv("IKG_PRESCAN");
   return e ? atoi(e) != 0 : B <= 65536;
+}
+static int box_cover() {
+  const char* e = getenv("IKG_BOX_COVER");
+  return e ? atoi(e) != 0 : 1;
 }
 static int64_t scan_waves(int64_t B) {
   const char* e = getenv("IKG_SCAN_WAVES");
@@ -1619,8 +1631,10 @@ __device__ inline bool witness_hit_lane(const KModel<T>* __restrict__ m, const K
 // each, lane 0 composes, then every lane runs the point search from its own
 // start (deep_point_from) and the deepest point (lowest start on a tie, as
 // deep_common_point) is the certificate's.  Wave-uniform; ends synchronised.
+// (inlined at each of its call sites: out of line, the call made the scan's
+// registers the callee's and the scan kernels fell from 3 waves per SIMD to 2)
 template <typename T>
-__device__ inline void scan_ball_cert(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c, int pair,
+__device__ __forceinline__ void scan_ball_cert(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c, int pair,
                                       const T* __restrict__ q, const int32_t* sl, const int32_t* par, const T* tgt,
                                       BallCert<T>& bc, T (*Lt)[12], unsigned long long* pc = nullptr) {
   const int lane = threadIdx.x;
@@ -1676,7 +1690,127 @@ __device__ inline void scan_ball_cert(const KModel<T>* __restrict__ m, const KCo
 #endif
 }
 
+// Does the certificate prove every iterate of window w colliding?  Its
+// iterates lie within L (the window's path length, per arm) of its first one
+// in every arm joint (ikg_solve.hpp kWin), so |q_k - qc_k| <= |first_k - qc_k|
+// + L for each; ball_covers' motion bound over that box (L widened by 1e-4 for
+// the rounding of its sum).  Passive joints: constant after the first update.
+// The certificate's columns are record slots (built on a record-layout row).
 template <typename T>
+__device__ inline bool box_covers(const BallCert<T>& bc, const T* __restrict__ cw, const T* PVr, const T* PVc,
+                                  bool first_it) {
+  const T L0 = cw[kCkL], L1 = cw[kCkArm + kCkL];
+  T s0[2] = {T(0), T(0)}, s1[2] = {T(0), T(0)};
+  for (int e = 0; e < bc.n; ++e) {
+    const int rs = bc.off[e];
+    T cv, hw;
+    if (rs < kRecPass) {
+      cv = cw[rs];
+      hw = L0;
+    } else if (rs < kRecPassive) {
+      cv = cw[kCkArm + rs - kRecPass];
+      hw = L1;
+    } else {
+      const int pi = rs - kRecPassive;
+      cv = first_it ? PVr[pi] : PVc[pi];
+      hw = first_it ? fabs(PVc[pi] - PVr[pi]) : T(0);
+    }
+    const T d = fabs(cv - bc.qc[e]) + hw * T(1.0001);
+    const int h = bc.side[e];
+    s0[h] += d;
+    s1[h] += d * bc.lev[e];
+  }
+  return bc.r > T(0) && s1[0] + bc.r * s0[0] < bc.r && s1[1] + bc.r * s0[1] < bc.r;
+}
+
+// Round -2, a converged problem that collides at its first passing iterate
+// (W.pair the pair found there).  A certificate for that pair at that
+// iterate, every window's box tested against it (64 windows at a time); then,
+// at the first window left, a certificate at its first iterate (a checkpoint:
+// an iterate of the loop) and the windows left tested again -- up to
+// kCoverCerts certificates.  All proved: every later passing iterate
+// collides, so the answer is the iterate after max_iters with success = False
+// (inverse_geometry.py:70, :97-98), from the final record.  Else the problem
+// is listed (wit_out) with the windows left (wmask) for the resume launch and
+// the records scan.  Wave-uniform; ends synchronised.
+constexpr int kCoverCerts = 1;
+constexpr int kCoverChunks = 4;  // windows tested: up to 64 x 4 (max_iters < 8,192); beyond, all left to the scan
+template <typename T>
+__device__ inline void window_covers(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
+                                     CollideScratch<T>& S, const T* tgt, const Witness<T>& W, const int32_t* SL,
+                                     BallCert<T>& BC, const TrajWs<T>& w, int64_t p, T* __restrict__ q_out,
+                                     uint8_t* __restrict__ conv, int32_t* __restrict__ iters, T* __restrict__ err) {
+  __shared__ T PVr[kMaxNq], PVc[kMaxNq];  // passive joints: the first passing iterate's values, and every later one's
+  __shared__ T RQ[kRecPassive + kMaxNq];  // the row a certificate is built at (record layout)
+  const int lane = threadIdx.x, nq = m->nq, npv = m->n_passive;
+  const int k0 = iters[p];
+  const int nrec = w.nrec[p] & ~kTrajEnded;
+  const int max_iters = k0 + nrec - 1;
+  const int nwp = (nrec + kWin - 1) / kWin;
+  const T* ckp = w.ck + p * ck_per_problem(max_iters);
+  if (lane < npv) {
+    const int pj = m->passive_q[lane];
+    const T v = q_out[p * nq + pj];
+    PVr[lane] = v;
+    PVc[lane] = clampq(v, m->lo[pj], m->hi[pj]);
+  }
+  bool open[kCoverChunks];
+#pragma unroll
+  for (int k = 0; k < kCoverChunks; ++k) open[k] = lane + 64 * k < nwp;
+  const bool boxes = w.box && nwp <= 64 * kCoverChunks;
+  for (int wt = 0, nc = 0; boxes && nc < kCoverCerts; ++nc) {  // wt: wave-uniform
+    const T* ct = ckp + (int64_t)wt * kCkSlot;
+    __syncthreads();  // RQ, BC, S.L free (the check, or the last round's tests, are done)
+    if (lane < kRecPass)
+      RQ[lane] = ct[kCkQ + lane];
+    else if (lane < kRecPassive)
+      RQ[lane] = ct[kCkArm + kCkQ + lane - kRecPass];
+    else if (lane < kRecPassive + npv)
+      RQ[lane] = k0 + wt * kWin > 0 ? PVc[lane - kRecPassive] : PVr[lane - kRecPassive];
+    __syncthreads();
+    scan_ball_cert(m, c, W.pair, RQ, SL, S.par, tgt, BC, S.L);
+    const bool ok = BC.r > T(0);  // wave-uniform (LDS)
+    int nxt = -1;
+#pragma unroll
+    for (int k = 0; k < kCoverChunks; ++k) {
+      const int wi = lane + 64 * k;
+      if (ok && open[k]) open[k] = !box_covers(BC, ckp + (int64_t)wi * kCkSlot, PVr, PVc, k0 + wi * kWin == 0);
+      const unsigned long long b = __ballot(open[k] && wi > wt);
+      if (nxt < 0 && b) nxt = 64 * k + __ffsll((long long)b) - 1;
+    }
+    if (nxt < 0) break;
+    wt = nxt;
+  }
+  bool any = false;
+  uint32_t* wm = w.wmask + p * mask_words(max_iters);
+  const int nmw = mask_words(max_iters);
+#pragma unroll
+  for (int k = 0; k < kCoverChunks; ++k) {
+    const unsigned long long b = __ballot(boxes ? open[k] : lane + 64 * k < nwp);
+    any = any || b != 0;
+    if (lane < 2 && 2 * k + lane < nmw) wm[2 * k + lane] = (uint32_t)(b >> (32 * lane));
+  }
+  for (int k = 2 * kCoverChunks + lane; k < nmw; k += 64) wm[k] = ~0u;  // windows past the tested ones
+  any = any || nmw > 2 * kCoverChunks;
+  if (!any) {
+    const T* fr = ckp + (int64_t)rec_windows(max_iters) * kCkSlot;
+    if (lane < nq) {
+      const int rs = SL[lane];
+      q_out[p * nq + lane] = rs < kRecPassive ? fr[rs] : PVc[rs - kRecPassive];
+    }
+    if (lane < 2) err[p * 2 + lane] = sqrt(fr[lane ? kRecErr1 : kRecErr0]);
+    if (lane == 0) {
+      conv[p] = 0;
+      iters[p] = max_iters;
+    }
+  }
+  if (lane == 0) w.wit_out[p] = any ? W.pair : -1;
+  __syncthreads();
+}
+
+// FIRST: round -2 only (ikg_first_check_kernel: the first check and the window
+// boxes, none of the records scan's code, so its registers stay the check's)
+template <typename T, bool FIRST = false>
 __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
                                                const T* __restrict__ targets, int64_t S_per_target,
                                                const int32_t* __restrict__ clist, int n,
@@ -1705,7 +1839,10 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     // answered by an earlier scan: window r - 1's, or (no pre-screen: witness0
     // null) the first checks' before window 0
     if ((round > 0 || (round == 0 && !witness0)) && w.done[i]) continue;  // wave-uniform
-    const bool fused = round == -2;  // first check, then (colliding) this problem's records
+    if constexpr (FIRST) round = -2;
+    // FIRST: every problem of the batch (its first check, then the window
+    // boxes), or with witness0 the pre-screen's colliding list (boxes only)
+    const bool fused = FIRST && !witness0;
     const int64_t p = fused ? (int64_t)i : (int64_t)clist[i];
     if (fused && !conv[p]) {  // wave-uniform
       if (lane == 0) w.wit_out[p] = -1;
@@ -1715,7 +1852,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     if (lane < 12) tgt[lane] = targets[t_idx * 12 + lane];
     if (lane < nq) S.par[lane] = m->jparent[lane];
     if (lane == 0) {  // the pre-screen's colliding pair, else the one the last window ended with
-      const int wp0 = round < 0 ? -1 : (witness0 && round == 0) ? witness0[p] : w.cst[i].pair;
+      const int wp0 = fused || (round < 0 && !FIRST) ? -1 : witness0 && (round == 0 || FIRST) ? witness0[p] : w.cst[i].pair;
       W.pair = wp0 >= 0 && wp0 < c->n_pairs ? wp0 : -1;  // a witness is only a hint: never trust an index
       W.cert_ok = 0;
       bc_pair = -1;
@@ -1724,19 +1861,24 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     if (round < 0 && lane < nq) S.q[lane] = q_out[p * nq + lane];
     __syncthreads();
     if (round < 0) {
-      stage_trig_par(m, S);
-      __syncthreads();
-      const bool col = collide_wave<T, true>(m, c, S, tgt, W);
+      bool col = true;  // FIRST over the pre-screen's list: colliding (W.pair the pair it found)
+      if (!FIRST || fused) {
+        stage_trig_par(m, S);
+        __syncthreads();
+        col = collide_wave<T, true>(m, c, S, tgt, W);
+      }
       if (lane == 0) {
-        if (fused)
-          w.wit_out[p] = col ? W.pair : -1;
+        if (FIRST)
+          w.wit_out[p] = -1;  // window_covers sets it when windows are left to regenerate
         else if (col)
           w.cst[i].pair = W.pair;
         else
           w.done[i] = 1;  // :70 errors pass and no collision: final as the batch kernel left it
       }
       __syncthreads();
-      if (!(fused && col)) continue;  // wave-uniform; fused + colliding: scan the records with this witness
+      if constexpr (FIRST)
+        if (col && W.pair >= 0) window_covers(m, c, S, tgt, W, SL, BC, w, p, q_out, conv, iters, err);
+      continue;  // wave-uniform
     }
     const int64_t ix = w.by_p ? p : par + i;
     const int nr = w.nrec[ix];
@@ -1754,6 +1896,12 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
 #else
     unsigned long long* pc = nullptr;
 #endif
+    // regenerated records (round 0 after round -2): only the windows the box
+    // tests left (wm), the others proved colliding
+    const uint32_t* wm = w.wmask ? w.wmask + p * mask_words(it0 + nrec - 1) : nullptr;
+    int rstart = 0;
+    if (wm)
+      while (rstart < nrec && !win_flagged(wm, rstart / kWin)) rstart += kWin;
     if (w.by_p) {  // the batch kernels record no passive joints: constant from the first update on
       // staged in LDS first: read from q_out inside the loop, they were reloaded
       // after every record store (q_out may alias the records), a memory round
@@ -1766,8 +1914,9 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
         S.cs[lane] = clampq(v, m->lo[pj], m->hi[pj]);  // every later one
       }
       __syncthreads();
-      for (int j = lane; j < nrec; j += 64)
-        for (int k = 0; k < npv; ++k) rec[(int64_t)j * RL + kRecPassive + k] = it0 + j > 0 ? S.cs[k] : S.sn[k];
+      for (int j = rstart + lane; j < nrec; j += 64)
+        if (!wm || win_flagged(wm, j / kWin))
+          for (int k = 0; k < npv; ++k) rec[(int64_t)j * RL + kRecPassive + k] = it0 + j > 0 ? S.cs[k] : S.sn[k];
       __syncthreads();
     }
     int ans = -1;
@@ -1781,13 +1930,14 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
 #ifdef IKG_CPROF
     pc[11] += clock64() - cp0;  // passive columns
 #endif
-    for (int start = 0; start < nrec && ans < 0; start += 64) {
+    for (int start = rstart; start < nrec && ans < 0; start += 64) {
 #ifdef IKG_CPROF
       const unsigned long long cc0 = clock64();
 #endif
       const int j = start + lane;
-      const T* r = rec + (int64_t)min(j, nrec - 1) * RL;
-      bool need = j < nrec && r[kRecPass] != T(0);
+      const bool live = j < nrec && (!wm || win_flagged(wm, j / kWin));  // a record regenerated
+      const T* r = rec + (int64_t)(live ? j : rstart) * RL;
+      bool need = live && r[kRecPass] != T(0);
       // inscribed-ball certificates of the witness pair: every lane's motion
       // bound against the current certificate (ball_covers) proves its record
       // colliding with no narrow phase; a new certificate (one lane's
@@ -1887,8 +2037,11 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
 #endif
     const int a = ans >= 0 ? ans : (ended ? nrec - 1 : -1);
     if (a >= 0) {  // final: the answer, or the iterate after max_iters (success = False)
-      const T* r = rec + (int64_t)a * RL;
-      if (lane < nq) q_out[p * nq + lane] = r[SL[lane]];
+      // the latter from the batch kernel's final record when its window was not regenerated
+      const bool fin = ans < 0 && wm && !win_flagged(wm, a / kWin);
+      const T* r = fin ? w.ck + p * ck_per_problem(it0 + nrec - 1) + (int64_t)rec_windows(it0 + nrec - 1) * kCkSlot
+                       : rec + (int64_t)a * RL;
+      if (lane < nq) q_out[p * nq + lane] = (fin && SL[lane] >= kRecPassive) ? S.cs[SL[lane] - kRecPassive] : r[SL[lane]];
       if (lane < 2) err[p * 2 + lane] = sqrt(r[lane ? kRecErr1 : kRecErr0]);
       if (lane == 0) {
         conv[p] = ans >= 0 ? 1 : 0;
@@ -1925,6 +2078,21 @@ void ikg_traj_update_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
                                                              int r) {
   traj_window<T, DAMPED, SP>(m, prm, targets, S_per_target, q_out, iters, clist, *count, w, Wn, r, (int)blockIdx.x,
                              (int)gridDim.x);
+}
+
+// Round -2 over the batch (one wave per problem, grid-stride): the first
+// check at the batch kernel's iterate and the window boxes (window_covers);
+// with witness0, over the pre-screen's colliding list (clist, *count): the
+// window boxes only
+template <typename T>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 3 : 1)))
+void ikg_first_check_kernel(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
+                            const T* __restrict__ targets, int64_t S_per_target, int64_t B,
+                            const int32_t* __restrict__ clist, const int32_t* __restrict__ count,
+                            const int32_t* __restrict__ witness0, TrajWs<T> w, T* __restrict__ q_out,
+                            uint8_t* __restrict__ conv, int32_t* __restrict__ iters, T* __restrict__ err) {
+  traj_scan_body<T, true>(m, c, targets, S_per_target, clist, count ? *count : (int)B, witness0, w, 0, -2, q_out, conv,
+                          iters, err, (int)blockIdx.x, (int)gridDim.x);
 }
 
 // fp32: at most 168 VGPRs, so 3 waves fit a SIMD as before the certificate
@@ -2197,60 +2365,89 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
   ws_trace("alloc cont", ws, 3 * ib + 256 + sizeof(T) * kStretchRec * (size_t)a.B, s);
   poison_int(ws, 3 * ib + 256, s);  // witness, lists, counts
   poison_float(w.rec, sizeof(T) * kStretchRec * (size_t)a.B, s);
-  // trajectory continuation without a pre-screen: the first checks run in its
-  // first launch, so every converged problem is listed
-  const bool first = !(a.rec_used && *a.rec_used) && cont_traj(a.B) && !traj_prescreen(a.B);
-  const bool fused = a.rec_used && *a.rec_used && prescan_on(a.B);
-  if (fused) {
-    // nothing here: the scan below checks every converged problem itself
-  } else if (first)
-    hipLaunchKernelGGL(ikg_mark_converged_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s,
-                       (const uint8_t*)a.converged, a.B, w.wit);
-  else
-    hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
-                       (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
-  if (!fused) {  // the chunk counts borrow the stretch list (written only after the compaction)
-    const unsigned nb = (unsigned)((a.B + kCompactChunk - 1) / kCompactChunk);
+  const bool damped = prm.lambda > T(0);
+  hipError_t ec = hipSuccess;
+  const unsigned nb = (unsigned)((a.B + kCompactChunk - 1) / kCompactChunk);
+  auto compact = [&] {  // listed: witness >= 0 (the chunk counts borrow the stretch list, written only after)
     hipLaunchKernelGGL(ikg_compact_count_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)w.wit, a.B, w.list);
     hipLaunchKernelGGL(ikg_compact_write_kernel, dim3(nb), dim3(256), 0, s, (const int32_t*)w.wit, a.B,
                        (const int32_t*)w.list, w.clist, w.count + 1);
-  }
-  const bool damped = prm.lambda > T(0);
-  hipError_t ec = hipSuccess;
-  if (a.rec_used && *a.rec_used) {  // the pair kernel recorded every iterate from the first passing one
+  };
+  if (a.rec_used && *a.rec_used) {
+    // the batch kernel wrote window checkpoints from each problem's first
+    // passing iterate (ikg_solve.hpp kWin): (1) one wave per problem of the
+    // batch checks it there and, when it collides, tests every window's box
+    // against a certificate at that iterate (round -2); (2) the problems with
+    // a window left are listed; (3) the batch kernel regenerates their
+    // records from that window on (resume launch); (4) the records scan
+    const size_t bi = ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255);
+    const size_t bm = ((sizeof(uint32_t) * (size_t)mask_words(prm.max_iters) * (size_t)a.B + 255) & ~(size_t)255);
+    const size_t bc = ((sizeof(TrajCert<T>) * (size_t)a.B + 255) & ~(size_t)255);
     char* dws = nullptr;
-    e = ws_alloc(a.ws_owner, (void**)&dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
+    e = ws_alloc(a.ws_owner, (void**)&dws, bi + bm + bc, s);
     if (e != hipSuccess) return e;
     TrajWs<T> tw{};
     tw.rec = (T*)a.rec;
     tw.nrec = a.rec_n;
     tw.it0 = a.iters;
     tw.done = (int32_t*)dws;
-    tw.cst = (TrajCert<T>*)(dws + ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255));
+    tw.wmask = (uint32_t*)(dws + bi);
+    tw.cst = (TrajCert<T>*)(dws + bi + bm);
     tw.slots = a.B;
     tw.by_p = 1;
     tw.cert = scan_cert();
-    ws_trace("alloc scan", dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
-    poison_int(dws, (sizeof(int32_t) + sizeof(TrajCert<T>)) * (size_t)a.B + 256, s);
-    // one scan round with the pre-screen's witnesses: `done` is only written
-    // (read by later rounds, of which there are none here), so it needs no fill
-    if (fused) {  // one wave per problem of the batch: its first check, then its records if it collides
-      tw.wit_out = w.wit;
-      hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)std::min<int64_t>(a.B, int64_t(1) << 20)), dim3(64),
-                         0, s, dm, dc, (const T*)a.targets, a.S, (const int32_t*)nullptr, (const int32_t*)nullptr,
-                         (const int32_t*)nullptr, tw, prm.max_iters + 1, -2, (T*)a.q_out, a.converged, a.iters,
+    tw.ck = (const T*)a.ck;
+    tw.box = box_cover();
+    ws_trace("alloc scan", dws, bi + bm + bc, s);
+    poison_int(dws, bi + bm + bc, s);
+    // `done` is only written (read by later rounds, of which there are none here), so it needs no fill
+    tw.wit_out = w.wit;
+    if (first_fused(a.B)) {
+      hipLaunchKernelGGL((ikg_first_check_kernel<T>), dim3((unsigned)std::min<int64_t>(a.B, int64_t(1) << 20)), dim3(64),
+                         0, s, dm, dc, (const T*)a.targets, a.S, a.B, (const int32_t*)nullptr,
+                         (const int32_t*)nullptr, (const int32_t*)nullptr, tw, (T*)a.q_out, a.converged, a.iters,
                          (T*)a.err_out);
-    } else {
+    } else {  // pre-screen, its colliding list, the window boxes over it (rewriting w.wit in place)
+      hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
+                         (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
+      compact();
+      hipLaunchKernelGGL((ikg_first_check_kernel<T>), dim3((unsigned)scan_waves(a.B)), dim3(64), 0, s, dm, dc,
+                         (const T*)a.targets, a.S, a.B, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
+                         (const int32_t*)w.wit, tw, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out);
+    }
+    compact();
+    BatchArgs r = a;
+    r.rec_list = w.clist;
+    r.rec_count = w.count + 1;
+    r.rec_wmask = tw.wmask;
+    ec = launch_pair_batch<T>(dm, prm, r, spec, s);
+    if (ec == hipSuccess) {
+      tw.wit_out = nullptr;
       hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)scan_waves(a.B)), dim3(64), 0, s, dm, dc,
                          (const T*)a.targets, a.S, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
                          (const int32_t*)w.wit, tw, prm.max_iters + 1, 0, (T*)a.q_out, a.converged, a.iters,
                          (T*)a.err_out);
+      ec = hipGetLastError();
     }
-    ec = hipGetLastError();
     ws_trace("free scan", dws, 0, s);
     const hipError_t ef2 = ws_free(a.ws_owner, dws, s);
     if (ec == hipSuccess) ec = ef2;
-  } else if (spec == kSpecNextage) {
+    e = ec != hipSuccess ? ec : hipGetLastError();
+    ws_trace("free cont", ws, 0, s);
+    const hipError_t ef = ws_free(a.ws_owner, ws, s);
+    return e != hipSuccess ? e : ef;
+  }
+  // trajectory continuation without a pre-screen: the first checks run in its
+  // first launch, so every converged problem is listed
+  const bool first = cont_traj(a.B) && !traj_prescreen(a.B);
+  if (first)
+    hipLaunchKernelGGL(ikg_mark_converged_kernel, dim3((unsigned)((a.B + 255) / 256)), dim3(256), 0, s,
+                       (const uint8_t*)a.converged, a.B, w.wit);
+  else
+    hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
+                       (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
+  compact();
+  if (spec == kSpecNextage) {
     if (damped)
       launch_continue_sel<T, true, SpecNextage>(dm, dc, prm, a, nq, ng, w, s, ec, first);
     else

@@ -50,7 +50,7 @@ namespace ikg {
 template <typename T, bool DAMPED, class SP>
 constexpr int kPairMinWaves = (kFrame1<SP> && !DAMPED) ? (sizeof(T) == 8 ? IKG_PAIR_MINW64 : 4) : 1;
 
-template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
+template <typename T, bool DAMPED, class SP, bool MED = false, int REC = 0>
 __global__ __launch_bounds__(64)
 #if IKG_WPE
 __attribute__((amdgpu_waves_per_eu(1, IKG_WPE)))
@@ -63,13 +63,12 @@ void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             int64_t S, int ppw, T* __restrict__ q_out,
                                                             uint8_t* __restrict__ conv_out,
                                                             int32_t* __restrict__ iters_out,
-                                                            T* __restrict__ err_out, T* __restrict__ rec = nullptr,
-                                                            int32_t* __restrict__ rec_n = nullptr) {
+                                                            T* __restrict__ err_out, RecArgs<T> ra = RecArgs<T>{}) {
   // model tables stay in global memory: the compiler hoists them into
   // registers (staging them in LDS and re-reading per iteration measured 8%
   // slower)
   pair_batch_body<T, DAMPED, SP, MED, REC>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out, iters_out,
-                                           err_out, rec, rec_n);
+                                           err_out, ra);
 }
 
 
@@ -256,16 +255,31 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
         (void)launch_pair_ilp(dmodel, prm, a, med, lds_pad_bytes(), s);
         return;
       }
-    if (a.rec) {  // collision continuation records (ikg_collision.hip), one fixed slot per problem
+    if (a.rec) {  // collision continuation checkpoints (ikg_collision.hip), one fixed slot per problem
+      RecArgs<T> ra;
+      ra.rec = (T*)a.rec;
+      ra.nrec = a.rec_n;
+      ra.ck = (T*)a.ck;
+      ra.list = a.rec_list;
+      ra.count = a.rec_count;
+      ra.wmask = a.rec_wmask;
+      // resume (a.rec_list): the same kernel over (listed problem, window) tasks, grid-stride
+      const dim3 g = a.rec_list ? dim3(resume_waves(a.B, rec_windows(prm.max_iters), ppw)) : grid;
       auto go = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, dim3(64), lds_pad_bytes(), s, dmodel, prm, (const T*)a.targets,
+        hipLaunchKernelGGL(kern, g, dim3(64), lds_pad_bytes(), s, dmodel, prm, (const T*)a.targets,
                            (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out, a.converged, a.iters,
-                           (T*)a.err_out, (T*)a.rec, a.rec_n);
+                           (T*)a.err_out, ra);
       };
-      if (med)
-        go(ikg_pair_batch_kernel<T, DAMPED, SP, true, true>);
-      else
-        go(ikg_pair_batch_kernel<T, DAMPED, SP, false, true>);
+      if (a.rec_list) {  // the resume kernel (REC = 2)
+        if (med)
+          go(ikg_pair_batch_kernel<T, DAMPED, SP, true, 2>);
+        else
+          go(ikg_pair_batch_kernel<T, DAMPED, SP, false, 2>);
+      } else if (med) {
+        go(ikg_pair_batch_kernel<T, DAMPED, SP, true, 1>);
+      } else {
+        go(ikg_pair_batch_kernel<T, DAMPED, SP, false, 1>);
+      }
       if (a.rec_used) *a.rec_used = true;
       return;
     }
@@ -400,6 +414,7 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   b.jit = a.jit;
   b.rec = a.rec;
   b.rec_n = a.rec_n;
+  b.ck = a.ck;
   b.rec_used = a.rec_used;
   // AUTO keeps the pair layout here: seeds spread the update counts, and a
   // wave lasts as long as its slowest problem -- 64 per packed wave against 32

@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
 #include <utility>
@@ -273,9 +274,21 @@ struct BatchArgs {
   // when the launch took them
   void* rec = nullptr;
   int32_t* rec_n = nullptr;
+  void* ck = nullptr;           // window checkpoints (ikg_solve.hpp kWin), ck_per_problem per problem
   bool* rec_used = nullptr;
+  // resume launch (the collision scan's windows to regenerate, ikg_collision.hip):
+  // listed problems, their count (device) and windows to regenerate per problem
+  const int32_t* rec_list = nullptr;
+  const int32_t* rec_count = nullptr;
+  const uint32_t* rec_wmask = nullptr;
   WsOwner* ws_owner = nullptr;  // scratch of captured solves (ws_alloc)
 };
+
+// waves of a resume launch (grid-stride over listed problems x windows)
+inline unsigned resume_waves(int64_t B, int nw, int per_wave) {
+  const int64_t w = (B * nw + per_wave - 1) / per_wave;
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(w, 4096));
+}
 
 struct MultiArgs {
   const void* targets;
@@ -303,6 +316,7 @@ struct MultiArgs {
   // collision continuation records for the S x T per-seed problems (BatchArgs::rec)
   void* rec = nullptr;
   int32_t* rec_n = nullptr;
+  void* ck = nullptr;
   bool* rec_used = nullptr;
   int64_t rec_chunk = 0;  // targets per launch when the records of all T x S problems exceed the budget (0: all)
 };

@@ -31,10 +31,13 @@ namespace ikg {
 // (amdgpu_waves_per_eu bounds the allocation at the occupancy the cap allows;
 // the guarded step's LQ branch is an out-of-line call, and its spills and
 // stack frame are touched only when it is taken -- DESIGN.md §3a.5)
-// REC: the collision continuation's records (ikg_collision.hip §3b), written
-// from the first passing iterate on, both arms' blocks by the problem's lane;
-// the outputs at that iterate come from its record 0 (solve_pair).
-template <class SP, int WPS, bool MED, bool REC = false>
+// REC = 1: the collision continuation's window checkpoints (ikg_solve.hpp
+// kWin), written from the first passing iterate on, both arms' by the
+// problem's lane; the outputs at that iterate come from window 0's checkpoint
+// (solve_pair).  REC = 2, the resume launch: one lane per (listed problem,
+// window) task, grid-stride, restarting at the window's checkpoint and
+// recording it (the same loop as its own instantiation, solve_pair).
+template <class SP, int WPS, bool MED, int REC = 0>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPS == 0 ? 3 : WPS)))
 void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               KParams<float> prm, const float* __restrict__ targets,
@@ -42,13 +45,44 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
                                                               int64_t B, int64_t S, float* __restrict__ q_out,
                                                               uint8_t* __restrict__ conv_out,
                                                               int32_t* __restrict__ iters_out,
-                                                              float* __restrict__ err_out, float* __restrict__ rec = nullptr,
-                                                              int32_t* __restrict__ rec_n = nullptr) {
+                                                              float* __restrict__ err_out,
+                                                              RecArgs<float> ra = RecArgs<float>{}) {
   if constexpr (WPS == 1) asm volatile("" ::: "a255");
   // v171: at least 172 VGPRs, so 2 waves fit and 3 do not; an AGPR claim
   // instead makes the allocator split the 2-wave budget 128 VGPR / 128 AGPR
   // and spill the loop (with the guarded step's cold branch in the kernel)
   if constexpr (WPS == 2) asm volatile("" ::: "v171");
+  if constexpr (REC == 2) {
+    const int nw = rec_windows(prm.max_iters);
+    const int64_t ntask = (int64_t)(*ra.count) * nw;
+    const int rl = rec_len(m->n_passive);
+    for (int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x; t < ntask; t += (int64_t)gridDim.x * 64) {
+      const int64_t i = t / nw;
+      const int w = (int)(t - i * nw);
+      const int64_t p = ra.list[i];
+      const int nr = ra.nrec[p] & ~kTrajEnded;
+      if (w * kWin >= nr || !win_flagged(ra.wmask + p * mask_words(prm.max_iters), w)) continue;
+      const int k0 = iters_out[p];
+      const int64_t tgt = S > 1 ? p / S : p;
+      const int64_t row = S > 1 ? p - tgt * S : p;
+      v2f RT[9], tT[3];
+      hook_target_packed(m, targets + tgt * 12, RT, tT);
+      float* ckw = ra.ck + p * ck_per_problem(prm.max_iters) + (int64_t)w * kCkSlot;
+      v2f qc = v2f{ckw[kCkQ], ckw[kCkArm + kCkQ]}, qa[kArmDof];
+#pragma unroll
+      for (int k = 0; k < kArmDof; ++k) qa[k] = v2f{ckw[kCkQ + 1 + k], ckw[kCkArm + kCkQ + 1 + k]};
+      RecOut<float> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
+                       q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl, ckw};
+      ro.k0 = k0;
+      ro.it_start = k0 + w * kWin;
+      ro.it_stop = k0 + min((w + 1) * kWin, nr);
+      int it;
+      bool conv;
+      v2f nrm, other;
+      solve_pair<v2f, false, SP, MED, 2>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro);
+    }
+    return;
+  }
   const int64_t p = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (p >= B) return;
   const int64_t tgt = S > 1 ? p / S : p;
@@ -62,12 +96,13 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
   int it;
   bool conv;
   v2f nrm, other;
-  if constexpr (REC) {
+  if constexpr (REC == 1) {
     const int rl = rec_len(m->n_passive);
-    RecOut<float> ro{rec + p * (int64_t)(prm.max_iters + 1) * rl, rec_n + p, qrow,
-                     q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl};
-    rec_n[p] = 0;
-    if (solve_pair<v2f, false, SP, MED, true>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
+    RecOut<float> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, qrow,
+                     q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl,
+                     ra.ck + p * ck_per_problem(prm.max_iters)};
+    ra.nrec[p] = 0;
+    if (solve_pair<v2f, false, SP, MED, 1>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
     solve_pair<v2f, false, SP, MED>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other);
   }
@@ -119,7 +154,7 @@ static unsigned simd_count() {
 
 // The cap instantiation really fits WPS waves per SIMD (4 WPS single-wave
 // workgroups per CU) on this device; otherwise the uncapped kernel runs.
-template <int WPS, bool REC = false>
+template <int WPS, int REC = 0>
 static bool capped_ok() {
   constexpr int kDevs = 64;
   static std::atomic<int> cache[kDevs];  // 0 unknown, 1 ok, 2 not
@@ -141,21 +176,31 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
   const dim3 grid((unsigned)((a.B + 63) / 64));
   const unsigned simds = simd_count();
   const unsigned need = (grid.x + simds - 1) / simds;  // waves per SIMD the launch needs
+  RecArgs<float> ra;
+  ra.rec = (float*)a.rec;
+  ra.nrec = a.rec_n;
+  ra.ck = (float*)a.ck;
+  ra.list = a.rec_list;
+  ra.count = a.rec_count;
+  ra.wmask = a.rec_wmask;
+  // resume (a.rec_list): the instantiation the batch launch took (need from a.B), grid-stride over tasks
+  const dim3 g = a.rec_list ? dim3(resume_waves(a.B, rec_windows(prm.max_iters), 64)) : grid;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, grid, dim3(64), packed_lds_pad(), s, dmodel, prm, (const float*)a.targets,
+    hipLaunchKernelGGL(kern, g, dim3(64), packed_lds_pad(), s, dmodel, prm, (const float*)a.targets,
                        (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out, a.converged, a.iters,
-                       (float*)a.err_out, (float*)a.rec, a.rec_n);
+                       (float*)a.err_out, ra);
   };
 #ifndef IKG_PACKED_REC
 #define IKG_PACKED_REC 1
 #endif
-  if (IKG_PACKED_REC && a.rec) {  // collision continuation records (0: A/B knob, the trajectory kernel instead)
-    if (need == 1 && capped_ok<1, true>())
-      go(ikg_packed_batch_kernel<SpecNextage, 1, true, true>);
-    else if (need == 2 && capped_ok<2, true>())
-      go(ikg_packed_batch_kernel<SpecNextage, 2, true, true>);
+  if (IKG_PACKED_REC && a.rec) {  // collision continuation checkpoints (0: A/B knob, the trajectory kernel instead)
+    // the resume launch (a.rec_list, REC = 2) takes the cap the batch launch took (need from a.B)
+    if (need == 1 && capped_ok<1, 1>())
+      a.rec_list ? go(ikg_packed_batch_kernel<SpecNextage, 1, true, 2>) : go(ikg_packed_batch_kernel<SpecNextage, 1, true, 1>);
+    else if (need == 2 && capped_ok<2, 1>())
+      a.rec_list ? go(ikg_packed_batch_kernel<SpecNextage, 2, true, 2>) : go(ikg_packed_batch_kernel<SpecNextage, 2, true, 1>);
     else
-      go(ikg_packed_batch_kernel<SpecNextage, 0, true, true>);
+      a.rec_list ? go(ikg_packed_batch_kernel<SpecNextage, 0, true, 2>) : go(ikg_packed_batch_kernel<SpecNextage, 0, true, 1>);
     if (a.rec_used) *a.rec_used = true;
     return hipGetLastError();
   }

@@ -28,7 +28,7 @@ void ikg_pair_ilp_kernel(const KModel<float>* __restrict__ gm, KParams<float> pr
                          float* __restrict__ q_out, uint8_t* __restrict__ conv_out, int32_t* __restrict__ iters_out,
                          float* __restrict__ err_out) {
   pair_batch_body<float, false, SpecNextage, MED, false>(gm, prm, targets, q0, q0_stride, B, S, ppw, q_out, conv_out,
-                                                         iters_out, err_out, nullptr, nullptr);
+                                                         iters_out, err_out);
 }
 
 hipError_t launch_pair_ilp(const KModel<float>* dmodel, const KParams<float>& prm, const BatchArgs& a, bool med,

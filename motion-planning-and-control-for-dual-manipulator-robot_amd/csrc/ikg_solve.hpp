@@ -76,9 +76,64 @@ __device__ __forceinline__ void load_block8(const T* src, T (&v)[8]) {
   }
 }
 
-// Record-in-batch outputs of one problem (ikg_pair_batch_kernel with REC):
-// the loop goes on past the first iterate whose errors pass, recording every
-// iterate for the collision scan; that iterate's outputs are stored when reached.
+template <typename T>
+__device__ __forceinline__ void store_block4(T* dst, const T (&v)[4]) {
+  struct alignas(16) V16 {
+    T x[16 / sizeof(T)];
+  };
+  constexpr int per = 16 / (int)sizeof(T);
+#pragma unroll
+  for (int k = 0; k < 4 / per; ++k) {
+    V16 b;
+#pragma unroll
+    for (int e = 0; e < per; ++e) b.x[e] = v[k * per + e];
+    reinterpret_cast<V16*>(dst)[k] = b;
+  }
+}
+
+// ---- window checkpoints (round 6: the records' window form)
+// The batch kernel no longer writes every iterate past the first passing one
+// (k0): it writes, every kWin iterates from k0 on, a checkpoint of the loop's
+// whole state (q, the carried trig and rotation-angle values) and the window's
+// path length L (the sum over its updates of the largest joint step), and at
+// the end the record of the iterate after max_iters.  Every iterate of window
+// w lies within L_w of the window's first iterate in every joint, so the scan
+// proves a whole window colliding with one certificate test on that box
+// (ikg_collision.hip round -3); a window the box test does not prove is
+// regenerated from its checkpoint by the same kernel (RecArgs::list, "resume"),
+// bit for bit the iterates the batch loop ran, into the records the scan reads.
+// Slot layout per problem: (rec_windows + 1) slots of kCkSlot values; window w
+// in slot w, the final record (record layout, passive joints not filled) in
+// the last.  Within a slot, per arm (pair layout: the arm's lane; packed: the
+// arm's half) at arm * kCkArm:
+//   [0, 8)   root, the arm's joints, |e|^2   (the record block layout)
+//   [8, 15)  sn[0..6]      [16, 23) cs[0..6]
+//   [24, 27) rotation-angle track (fp64 pair layout)   [28] L
+constexpr int kWin = 32;  // iterates per window
+constexpr int kCkArm = 32, kCkSlot = 64;
+constexpr int kCkQ = 0, kCkSn = 8, kCkCs = 16, kCkTk = 24, kCkL = 28;
+IKG_HD inline int rec_windows(int max_iters) { return (max_iters + 1 + kWin - 1) / kWin; }
+IKG_HD inline int64_t ck_per_problem(int max_iters) { return (int64_t)(rec_windows(max_iters) + 1) * kCkSlot; }
+// the windows the scan could not prove colliding (regenerated and scanned):
+// one bit per window, mask_words 32-bit words per problem
+IKG_HD inline int mask_words(int max_iters) { return (rec_windows(max_iters) + 31) / 32; }
+IKG_HD inline bool win_flagged(const uint32_t* wm, int w) { return (wm[w >> 5] >> (w & 31)) & 1u; }
+
+// Kernel argument of the record-writing (REC) batch kernels.
+template <typename T>
+struct RecArgs {
+  T* rec = nullptr;                 // regenerated records: (max_iters + 1) x rec_len per problem
+  int32_t* nrec = nullptr;          // per problem: records from k0 (| kTrajEnded)
+  T* ck = nullptr;                  // window checkpoints: ck_per_problem per problem
+  const int32_t* list = nullptr;    // resume launch: the problems whose windows are regenerated (null: the batch solve)
+  const int32_t* count = nullptr;   // resume: list length (device)
+  const uint32_t* wmask = nullptr;  // resume: per problem, the windows to regenerate (mask_words each)
+};
+
+// Record-in-batch outputs of one problem (the REC batch kernels): the loop goes
+// on past the first iterate whose errors pass (k0), writing window checkpoints
+// for the collision scan; k0's outputs are stored from window 0's checkpoint.
+// resume: the loop restarts at window w's checkpoint and records its iterates.
 template <typename T>
 struct RecOut {
   T* rec;               // this problem's records, (max_iters + 1) x rec_len
@@ -89,6 +144,8 @@ struct RecOut {
   int32_t* iters;
   T* err;
   int rl;               // rec_len
+  T* ck;                // its checkpoint slots (resume: the window's)
+  int it_start = 0, k0 = -1, it_stop = 0;  // resume: first iterate, the problem's k0, one past the last iterate
 };
 
 // Diagnostic build only (-DIKG_STAGE_CLOCK, tools/stage_clock.py; no stamp
@@ -132,11 +189,54 @@ __device__ inline bool both_below(T x, T xo, E eps2) {
 // float: this lane owns one arm (pair layout, partner = lane ^ 1); T = v2f:
 // this lane owns both arms (packed layout).  Returns (through refs) the final
 // q of this lane, the update count and the hand error norms at the returned q.
-// REC: every iterate from the first passing one on is recorded into this
-// problem's fixed slot (ikg_capi.hip sizes the launches so the slots fit the
-// record budget: no shared state, so a problem's records and answer do not
-// depend on which other problems share the launch or in what order they run)
-template <typename T, bool DAMPED, class SP, bool MED = false, bool REC = false>
+// The per-arm values of a checkpoint: pair layout, this lane's arm at
+// arm * kCkArm; packed, arm 0 from .x and arm 1 from .y
+template <typename T>
+__device__ __forceinline__ T ck_get(const typename LaneT<T>::E* c, int arm, int off) {
+  if constexpr (is_packed<T>)
+    return T{c[off], c[kCkArm + off]};
+  else
+    return c[arm * kCkArm + off];
+}
+// writes v[0..N) at off of each arm (N = 4 or 8, 16-byte stores)
+template <typename T, int N>
+__device__ __forceinline__ void ck_put(typename LaneT<T>::E* c, int arm, int off, const T (&v)[N]) {
+  using E = typename LaneT<T>::E;
+  if constexpr (is_packed<T>) {
+    E a[N], b[N];
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+      a[k] = v[k].x;
+      b[k] = v[k].y;
+    }
+    if constexpr (N == 8) {
+      store_block8(c + off, a);
+      store_block8(c + kCkArm + off, b);
+    } else {
+      store_block4(c + off, a);
+      store_block4(c + kCkArm + off, b);
+    }
+  } else {
+    if constexpr (N == 8)
+      store_block8(c + arm * kCkArm + off, v);
+    else
+      store_block4(c + arm * kCkArm + off, v);
+  }
+}
+
+// REC = 1: from the first passing iterate on, the window checkpoints go into
+// this problem's fixed slots (ikg_capi.hip sizes the launches so the slots fit
+// the record budget: no shared state, so a problem's checkpoints and answer do
+// not depend on which other problems share the launch or in what order they
+// run).  REC = 2 (resume): the loop restarts at a checkpoint and records the
+// window's iterates, with a per-lane update count (a resume wave's tasks
+// restart at different iterates).  The two are separate instantiations of the
+// same source; the compiler contracts a few products into FMAs differently in
+// them, so a regenerated iterate agrees with the batch loop's to the last bits
+// of q (fp64 ~1e-16), not bit for bit.  One instantiation serving both was
+// bit-exact but made the batch kernel 33% slower (1,036 -> 1,382 us at C2:
+// register allocation around the resume branch), profiles/r06/records/.
+template <typename T, bool DAMPED, class SP, bool MED = false, int REC = 0>
 __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict__ m,
                                   const KParams<typename LaneT<T>::E>& prm, int arm, const T* RT, const T* tT, T& qc,
                                   T* qa, int& it_out, bool& conv_out, T& nrm_out, T& other_out,
@@ -146,15 +246,31 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   E* recp = REC ? ro->rec : nullptr;  // this problem's records
   static_assert(!(DAMPED && is_packed<T>), "the packed layout implements lambda = 0 only");
   constexpr bool F1 = kFrame1<SP> && !DAMPED;  // frame-1 path, its own trig slots
+  static_assert(!REC || F1, "records: the frame-1 loop only");
   T sn[7], cs[7];
-  if constexpr (F1)
-    trig_exact_f1(m, arm, qc, qa, sn, cs);
-  else
-    trig_exact(qc, qa, sn, cs);
   int it = 0;
+  ThetaTrack<T> tk{};
+  T L = T(0);  // REC: this window's path length (largest joint step per update, summed)
+  if constexpr (REC == 2) {  // the loop state at the checkpoint (qc, qa: the caller, from the same slot)
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      sn[j] = ck_get<T>(ro->ck, arm, kCkSn + j);
+      cs[j] = ck_get<T>(ro->ck, arm, kCkCs + j);
+    }
+    if constexpr (!is_packed<T>) {
+      tk.th = ck_get<T>(ro->ck, arm, kCkTk);
+      tk.st = ck_get<T>(ro->ck, arm, kCkTk + 1);
+      tk.ct = ck_get<T>(ro->ck, arm, kCkTk + 2);
+    }
+    it = ro->it_start;
+    k0 = ro->k0;
+  } else if constexpr (F1) {
+    trig_exact_f1(m, arm, qc, qa, sn, cs);
+  } else {
+    trig_exact(qc, qa, sn, cs);
+  }
   bool conv = false;
   T x, xo;  // squared error norms of this lane's hand and the partner's
-  ThetaTrack<T> tk{};
 #if IKG_LANE_LIMITS
   ArmLimits<T> lim;
   if constexpr (!is_packed<T>) load_limits(m, arm, lim);
@@ -183,7 +299,8 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 #if IKG_UNIFORM
     // every live lane of the wave has run the same number of updates, so the
     // count (and the resync / max_iters tests on it) is wave-uniform: scalar
-    if constexpr (!is_packed<T>) it = __builtin_amdgcn_readfirstlane(it);
+    // (not the resume kernels: their lanes restart at different iterates)
+    if constexpr (!is_packed<T> && REC != 2) it = __builtin_amdgcn_readfirstlane(it);
 #endif
     // fp32: atan2f is as cheap as the tracked angle (measured)
     ThetaTrack<T>* tkp = (IKG_THETA_TRACK && is_f64<T>) ? &tk : nullptr;
@@ -226,7 +343,8 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
         k0 = it;
         conv = true;
       }
-      if (k0 >= 0) {
+      // the record of iterate `it`: this lane's block(s) in the record layout
+      auto put_record = [&](E* dst) {
         if constexpr (is_packed<T>) {  // both arms' blocks from the one lane
           float b0[8], b1[8];
           b0[0] = qc.x;
@@ -238,7 +356,6 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
           }
           b0[7] = x.x;
           b1[7] = x.y;
-          float* dst = recp + (int64_t)(it - k0) * ro->rl;
           store_block8(dst + kRecRoot, b0);
           store_block8(dst + kRecPass, b1);
         } else {
@@ -247,7 +364,45 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 #pragma unroll
           for (int k = 0; k < kArmDof; ++k) blk[1 + k] = qa[k];
           blk[7] = x;
-          store_block8(recp + (int64_t)(it - k0) * ro->rl + (arm ? kRecPass : kRecRoot), blk);
+          store_block8(dst + (arm ? kRecPass : kRecRoot), blk);
+        }
+      };
+      if (k0 >= 0) {
+        const int j = it - k0;
+        if constexpr (REC == 2) {  // a regenerated window: every iterate's record
+          put_record(recp + (int64_t)j * ro->rl);
+          if (it + 1 >= ro->it_stop) break;
+        } else {
+          if (j % kWin == 0) {  // a window starts: the previous one's length, then this state
+            E* cw = ro->ck + (int64_t)(j / kWin) * kCkSlot;
+            const T z = T(0);
+            if (j > 0) {
+              const T lv[4] = {L, z, z, z};
+              ck_put<T, 4>(cw - kCkSlot, arm, kCkL, lv);
+            }
+            T qb[8];
+            qb[0] = qc;
+#pragma unroll
+            for (int k = 0; k < kArmDof; ++k) qb[1 + k] = qa[k];
+            qb[7] = x;
+            ck_put<T, 8>(cw, arm, kCkQ, qb);
+            const T sb[8] = {sn[0], sn[1], sn[2], sn[3], sn[4], sn[5], sn[6], z};
+            const T cb[8] = {cs[0], cs[1], cs[2], cs[3], cs[4], cs[5], cs[6], z};
+            ck_put<T, 8>(cw, arm, kCkSn, sb);
+            ck_put<T, 8>(cw, arm, kCkCs, cb);
+            if constexpr (!is_packed<T>) {
+              const T tb[4] = {tk.th, tk.st, tk.ct, z};
+              ck_put<T, 4>(cw, arm, kCkTk, tb);
+            }
+            L = z;
+          }
+          if (ended) {  // the last window's length, and the iterate after max_iters as a record
+            E* cw = ro->ck + (int64_t)(j / kWin) * kCkSlot;
+            const T z = T(0);
+            const T lv[4] = {L, z, z, z};
+            ck_put<T, 4>(cw, arm, kCkL, lv);
+            put_record(ro->ck + (int64_t)rec_windows(prm.max_iters) * kCkSlot);
+          }
         }
       }
       if (ended) break;
@@ -267,6 +422,12 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     sc_acc[2] += sc_t1 - sc_t0;
 #endif
     arm_update(m, arm, T(prm.dt), s, dq, qc, qa, limp);
+    if constexpr (REC == 1) {  // the window's path length: this update's largest joint step
+      T mv = fabs(qc - q_old[0]);
+#pragma unroll
+      for (int k = 0; k < kArmDof; ++k) mv = fmax(mv, fabs(qa[k] - q_old[k + 1]));
+      L = L + mv;
+    }
     ++it;
 #ifdef IKG_STAGE_CLOCK
     IKG_STAMP(sc_t0);
@@ -300,14 +461,15 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   if (any_of(ps == T(-12345.678))) it = -1;  // never true; keeps the padding live
 #endif
   if constexpr (REC) {
+    if constexpr (REC == 2) return true;  // records only: the scan writes the outputs
     if (k0 >= 0) {
-      // the outputs at the first passing iterate, from its record (this lane's
-      // own block of record 0): writing them inside the loop put a divergent
-      // branch into every update (records-in-batch kernel 4% slower)
+      // the outputs at the first passing iterate, from window 0's checkpoint
+      // (this lane's own q block): writing them inside the loop put a
+      // divergent branch into every update (records-in-batch kernel 4% slower)
       if constexpr (is_packed<T>) {
         float b[2][8], qa0[kArmDof];
-        load_block8(recp + kRecRoot, b[0]);
-        load_block8(recp + kRecPass, b[1]);
+        load_block8(ro->ck + kCkQ, b[0]);
+        load_block8(ro->ck + kCkArm + kCkQ, b[1]);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -320,7 +482,7 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
         *ro->nrec = (it - k0 + 1) | kTrajEnded;
       } else {
       T blk[8];
-      load_block8(recp + (arm ? kRecPass : kRecRoot), blk);
+      load_block8(ro->ck + arm * kCkArm + kCkQ, blk);
       T qa0[kArmDof];
 #pragma unroll
       for (int k = 0; k < kArmDof; ++k) qa0[k] = blk[1 + k];
@@ -345,16 +507,54 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 // model-specialised kernels ikg_jit.cpp compiles at run time with `m` pointing
 // at a constant copy of the model tables): one 64-lane wave per workgroup
 // holding `ppw` problems on lanes [0, 2 ppw).
-template <typename T, bool DAMPED, class SP, bool MED, bool REC = false>
+// REC = 1: the same, writing window checkpoints.  REC = 2, the resume launch:
+// tasks (listed problem i, window w), ppw per wave, grid-stride, each lane
+// pair restarting problem ra.list[i] at window w's checkpoint and recording
+// the windows ra.wmask flags.
+template <typename T, bool DAMPED, class SP, bool MED, int REC = 0>
 __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KParams<T>& prm,
                                        const T* __restrict__ targets, const T* __restrict__ q0, int64_t q0_stride,
                                        int64_t B, int64_t S, int ppw, T* __restrict__ q_out,
                                        uint8_t* __restrict__ conv_out, int32_t* __restrict__ iters_out,
-                                       T* __restrict__ err_out, T* __restrict__ rec = nullptr,
-                                       int32_t* __restrict__ nrec = nullptr) {
+                                       T* __restrict__ err_out, const RecArgs<T>& ra = RecArgs<T>{}) {
   const int lane = threadIdx.x;
-  const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
   const int arm = lane & 1;
+  if constexpr (REC == 2) {
+    const int nw = rec_windows(prm.max_iters);
+    const int64_t ntask = (int64_t)(*ra.count) * nw;
+    const int rl = rec_len(m->n_passive);
+    const int64_t ckpp = ck_per_problem(prm.max_iters);
+    for (int64_t t0 = (int64_t)blockIdx.x * ppw; t0 < ntask; t0 += (int64_t)gridDim.x * ppw) {
+      const int64_t t = t0 + (lane >> 1);
+      if (lane >= 2 * ppw || t >= ntask) continue;  // both lanes of a pair together
+      const int64_t i = t / nw;
+      const int w = (int)(t - i * nw);
+      const int64_t p = ra.list[i];
+      const int nr = ra.nrec[p] & ~kTrajEnded;
+      if (w * kWin >= nr || !win_flagged(ra.wmask + p * mask_words(prm.max_iters), w)) continue;
+      const int k0 = iters_out[p];
+      const int64_t tgt = S > 1 ? p / S : p;
+      const int64_t row = S > 1 ? p - tgt * S : p;
+      T RT[9], tT[3];
+      hook_target(m, arm, targets + tgt * 12, RT, tT);
+      T* ckw = ra.ck + p * ckpp + (int64_t)w * kCkSlot;
+      const T* cq = ckw + arm * kCkArm + kCkQ;
+      T qc = cq[0], qa[kArmDof];
+#pragma unroll
+      for (int k = 0; k < kArmDof; ++k) qa[k] = cq[1 + k];
+      RecOut<T> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
+                   q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl, ckw};
+      ro.k0 = k0;
+      ro.it_start = k0 + w * kWin;
+      ro.it_stop = k0 + min((w + 1) * kWin, nr);
+      int it;
+      bool conv;
+      T nrm, other;
+      solve_pair<T, DAMPED, SP, MED, 2>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro);
+    }
+    return;
+  }
+  const int64_t p = (int64_t)blockIdx.x * ppw + (lane >> 1);
   if (lane >= 2 * ppw || p >= B) return;  // both lanes of a pair leave together
   // multi-start (S > 1): problem p = (target p / S, seed p % S)
   const int64_t tgt = S > 1 ? p / S : p;
@@ -367,12 +567,12 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
   int it;
   bool conv;
   T nrm, other;
-  if constexpr (REC) {  // the continuation's records (ikg_collision.hip): outputs at the first passing iterate
+  if constexpr (REC == 1) {  // the continuation's checkpoints (ikg_collision.hip): outputs at the first passing iterate
     const int rl = rec_len(m->n_passive);
-    RecOut<T> ro{rec + p * (int64_t)(prm.max_iters + 1) * rl, nrec + p, qrow, q_out + p * m->nq,
-                 conv_out + p, iters_out + p, err_out + p * 2, rl};
-    if (arm == 0) nrec[p] = 0;
-    if (solve_pair<T, DAMPED, SP, MED, true>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
+    RecOut<T> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, qrow, q_out + p * m->nq,
+                 conv_out + p, iters_out + p, err_out + p * 2, rl, ra.ck + p * ck_per_problem(prm.max_iters)};
+    if (arm == 0) ra.nrec[p] = 0;
+    if (solve_pair<T, DAMPED, SP, MED, 1>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
     solve_pair<T, DAMPED, SP, MED>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other);
   }

@@ -387,33 +387,80 @@ def _same_bits(a, b):
     return all(np.array_equal(x, y) for x, y in zip((a.q, a.converged, a.iters, a.err), (b.q, b.converged, b.iters, b.err)))
 
 
+def _close(a, b, tol):
+    """Same flags and update counts; q and the hand errors within tol."""
+    return (np.array_equal(a.converged, b.converged) and np.array_equal(a.iters, b.iters)
+            and np.abs(a.q.astype(np.float64) - b.q).max() <= tol
+            and np.abs(a.err.astype(np.float64) - b.err).max() <= tol)
+
+
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_record_chunks_give_the_one_launch_answer(csolver, dtype, monkeypatch):
     """VERDICT r5 item 1 / ADVICE r5: a collision solve whose records exceed
-    the budget runs in chunks whose fixed record slots fit it (ikg_capi.hip
+    the budget runs in chunks whose fixed slots fit it (ikg_capi.hip
     rec_chunk), never from a shared pool, so a problem's answer does not depend
     on the chunking or on wave order.  C2's 4,096 targets: one launch (the
-    default 24 GiB budget), and a 4 MB budget (fp64: 25 problems per launch,
-    fp32: 52) solved twice -- bit for bit equal.  Both first-check schedules
-    (IKG_PRESCAN=1: the check fused into the records scan, the default up to
-    65,536 problems per launch; 0: pre-screen + compaction + scan, the default
-    above) give the same bits too, with one launch and with chunks."""
+    default budget), and a 4 MB budget (fp64: 23 problems per launch, fp32: 47)
+    solved twice -- bit for bit equal; the same with every colliding problem's
+    records regenerated (IKG_BOX_COVER=0) and with the split first check
+    (IKG_PRESCAN=0: pre-screen + the window boxes over its list)."""
     from ikgrasp.workload import uniform_targets
     tg = uniform_targets(4096, seed=0)
     kw = dict(dtype=dtype, check_collision=True)
-    one = csolver.solve(tg, np.zeros(15), **kw)
-    monkeypatch.setenv("IKG_REC_BUDGET_MB", "4")
-    c1 = csolver.solve(tg, np.zeros(15), **kw)
-    c2 = csolver.solve(tg, np.zeros(15), **kw)
-    assert _same_bits(c1, c2)
-    assert _same_bits(one, c1)
-    for pre in ("0", "1"):
-        monkeypatch.setenv("IKG_PRESCAN", pre)
-        assert _same_bits(one, csolver.solve(tg, np.zeros(15), **kw)), ("chunks", pre)
-        monkeypatch.delenv("IKG_REC_BUDGET_MB")
-        assert _same_bits(one, csolver.solve(tg, np.zeros(15), **kw)), ("one launch", pre)
+    for env in ({}, {"IKG_BOX_COVER": "0"}, {"IKG_PRESCAN": "0"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        one = csolver.solve(tg, np.zeros(15), **kw)
         monkeypatch.setenv("IKG_REC_BUDGET_MB", "4")
+        c1 = csolver.solve(tg, np.zeros(15), **kw)
+        c2 = csolver.solve(tg, np.zeros(15), **kw)
+        assert _same_bits(c1, c2), env
+        assert _same_bits(one, c1), env
+        monkeypatch.delenv("IKG_REC_BUDGET_MB")
+        for k in env:
+            monkeypatch.delenv(k)
     assert 0 < int(one.converged.sum()) < 4096
+
+
+@pytest.mark.parametrize("case", ["f64", "f32", "packed", "multistart"])
+def test_window_boxes_agree_with_full_regeneration(csolver, solve_cases, monkeypatch, case):
+    """VERDICT r5 item 2 (round 6): the batch kernel writes a checkpoint per
+    32-iterate window from the first passing iterate on (ikg_solve.hpp kWin),
+    not every iterate; the scan proves a colliding problem's windows by one
+    certificate test on each window's box, and the windows it does not prove
+    are regenerated from their checkpoints (the resume kernel) and scanned
+    record by record.  IKG_BOX_COVER=0 proves no window, so every colliding
+    problem is regenerated in full -- the round-5 records' work.  A problem
+    whose windows are all proved takes the iterate after max_iters from the
+    batch kernel's final record, a regenerated one from the resume kernel's
+    records: the same loop compiled twice, so they agree to rounding (flags
+    and update counts equal, q within 1e-12 fp64 / 1e-5 fp32), and each is
+    deterministic (workspaces poisoned, solved twice).  Pair fp64, pair fp32,
+    the packed fp32 layout and a multi-start."""
+    from ikgrasp import _lib
+    from ikgrasp.workload import uniform_targets
+    monkeypatch.setenv("IKG_POISON", "1")
+    tg = uniform_targets(4096, seed=0)
+    tol = 1e-12 if case == "f64" or case == "multistart" else 1e-5
+    if case == "multistart":
+        c = solve_cases
+        seeds = np.stack([np.zeros(15)] + [c["q0"][-k] for k in range(1, 4)])
+        run = lambda: csolver.solve_multistart(tg[:1024], seeds, check_collision=True)
+    else:
+        kw = dict(dtype="f64" if case == "f64" else "f32", check_collision=True)
+        if case == "packed":
+            kw["variant"] = _lib.IKG_VARIANT_PACKED
+        run = lambda: csolver.solve(tg, np.zeros(15), **kw)
+    a = run()
+    assert _same_bits(a, run())
+    monkeypatch.setenv("IKG_BOX_COVER", "0")
+    b = run()
+    assert _same_bits(b, run())
+    assert _close(a, b, tol)
+    if case == "multistart":
+        assert np.array_equal(a.best_seed, b.best_seed)
+    else:
+        assert 0 < int(a.converged.sum()) < 4096
 
 
 def test_record_chunks_c3_fp32(csolver, monkeypatch):
@@ -447,10 +494,11 @@ def test_scan_certificates_do_not_change_answers(csolver, dtype, monkeypatch):
     """The records scan's inscribed-ball certificates (ikg_collision.hip
     scan_ball_cert / ball_covers) only skip narrow phases whose answer is
     "colliding": C2's 4,096 targets with the collision term give the same bits
-    with them (IKG_SCAN_CERT=1) and without (0), and they do prove records
-    here (the fixture's colliding passes)."""
+    with them (IKG_SCAN_CERT=1) and without (0), with every colliding problem's
+    records scanned (IKG_BOX_COVER=0, so the scan sees them all)."""
     from ikgrasp.workload import uniform_targets
     tg = uniform_targets(4096, seed=0)
+    monkeypatch.setenv("IKG_BOX_COVER", "0")
     out = {}
     for c in ("1", "0"):
         monkeypatch.setenv("IKG_SCAN_CERT", c)
