@@ -254,8 +254,13 @@ static size_t rec_budget() {
   return kRecBudgetMB << 20;
 }
 
+// the final record (record layout) fits a checkpoint slot (ikg_solve.hpp kCkSlot)
+static bool rec_fits(int nq) {
+  return ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof)) <= ikg::kCkSlot;
+}
+
 // bytes of one problem's record slot (the regenerated records) and window
-// checkpoints (ikg_solve.hpp kWin)
+// checkpoints (ikg_solve.hpp kWinOf)
 template <typename T>
 static size_t rec_records_bytes(const ikg_params& params, int nq) {
   const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
@@ -263,7 +268,7 @@ static size_t rec_records_bytes(const ikg_params& params, int nq) {
 }
 template <typename T>
 static size_t rec_slot_bytes(const ikg_params& params, int nq) {
-  return rec_records_bytes<T>(params, nq) + sizeof(T) * (size_t)ikg::ck_per_problem(params.max_iters);
+  return rec_records_bytes<T>(params, nq) + sizeof(T) * (size_t)ikg::ck_per_problem<T>(params.max_iters);
 }
 
 // units (problems, or multi-start targets of `per_unit` problems each) per
@@ -285,7 +290,7 @@ template <typename T>
 void* offer_records(ikg_model* model, ikg::BatchArgs& a, const ikg_params& params, int64_t n, int nq, hipStream_t s,
                     bool* rec_used) {
   const size_t b_rec = (rec_records_bytes<T>(params, nq) * (size_t)n + 255) & ~(size_t)255;
-  const size_t b_ck = (sizeof(T) * (size_t)ikg::ck_per_problem(params.max_iters) * (size_t)n + 255) & ~(size_t)255;
+  const size_t b_ck = (sizeof(T) * (size_t)ikg::ck_per_problem<T>(params.max_iters) * (size_t)n + 255) & ~(size_t)255;
   const size_t b_n = (sizeof(int32_t) * (size_t)n + 255) & ~(size_t)255;
   void* rec = nullptr;
   if (ikg::ws_alloc(&model->ws, &rec, b_rec + b_ck + b_n, s) != hipSuccess) {
@@ -366,7 +371,7 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   int64_t chunk = B;
   const ikg::KParams<T> kp = kparams<T>(params);
   if (dc && model->spec == ikg::kSpecNextage && !(params->lambda > 0) && !a.jit && rec_in_batch() &&
-      ikg::resolve_variant<T>(kp, model->spec, a.variant, B, true) != IKG_VARIANT_QUAD) {
+      rec_fits(nq) && ikg::resolve_variant<T>(kp, model->spec, a.variant, B, true) != IKG_VARIANT_QUAD) {
     chunk = rec_chunk<T>(*params, nq, B, 1);
     rec = offer_records<T>(model, a, *params, chunk, nq, s, &rec_used);
     if (!rec) chunk = B;
@@ -460,7 +465,7 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   bool rec_used = false;
   void* rec = nullptr;
   if (a.collision && model->spec == ikg::kSpecNextage && !(params->lambda > 0) && !a.jit && rec_in_batch() &&
-      params->variant != IKG_VARIANT_QUAD) {
+      rec_fits(nq) && params->variant != IKG_VARIANT_QUAD) {
     ikg::BatchArgs tmp{};
     a.rec_chunk = rec_chunk<T>(*params, nq, T_, S);  // targets per launch (each with its S seeds)
     rec = offer_records<T>(model, tmp, *params, a.rec_chunk * S, nq, s, &rec_used);

@@ -1392,7 +1392,7 @@ struct TrajWs {
   int64_t slots;      // slots per parity
   int by_p = 0;       // records, counts and it0 indexed by problem (the pair kernel's records)
   int cert = 1;       // inscribed-ball certificates before the witness tests (IKG_SCAN_CERT=0: off)
-  // round -2 (window checkpoints, ikg_solve.hpp kWin): problem i = index i of
+  // round -2 (window checkpoints, ikg_solve.hpp kWinOf): problem i = index i of
   // the batch, every converged one checked first, then a colliding one's
   // windows tested against certificates; wit_out[i] = the colliding pair
   // found when some window is left to regenerate (flagged in wmask), -1 if
@@ -1400,6 +1400,8 @@ struct TrajWs {
   int32_t* wit_out = nullptr;
   const T* ck = nullptr;        // the batch kernel's window checkpoints
   uint32_t* wmask = nullptr;    // per problem, the windows left (mask_words each): written by round -2, read by round 0
+  T* ctab = nullptr;            // per problem, round -2's certificate for the resume kernel (ikg_solve.hpp kCtab)
+  const uint64_t* rmask = nullptr;  // round 0: per problem and window, the iterates the resume kernel recorded
   int box = 1;                  // round -2: window boxes tested (IKG_BOX_COVER)
 };
 
@@ -1692,14 +1694,14 @@ __device__ __forceinline__ void scan_ball_cert(const KModel<T>* __restrict__ m, 
 
 // Does the certificate prove every iterate of window w colliding?  Its
 // iterates lie within L (the window's path length, per arm) of its first one
-// in every arm joint (ikg_solve.hpp kWin), so |q_k - qc_k| <= |first_k - qc_k|
+// in every arm joint (ikg_solve.hpp kWinOf), so |q_k - qc_k| <= |first_k - qc_k|
 // + L for each; ball_covers' motion bound over that box (L widened by 1e-4 for
 // the rounding of its sum).  Passive joints: constant after the first update.
 // The certificate's columns are record slots (built on a record-layout row).
 template <typename T>
 __device__ inline bool box_covers(const BallCert<T>& bc, const T* __restrict__ cw, const T* PVr, const T* PVc,
                                   bool first_it) {
-  const T L0 = cw[kCkL], L1 = cw[kCkArm + kCkL];
+  const T L0 = cw[kCkSlot + kCkL], L1 = cw[kCkSlot + kCkArm + kCkL];  // L_w: in slot w + 1 (never k0's slot)
   T s0[2] = {T(0), T(0)}, s1[2] = {T(0), T(0)};
   for (int e = 0; e < bc.n; ++e) {
     const int rs = bc.off[e];
@@ -1746,8 +1748,9 @@ __device__ inline void window_covers(const KModel<T>* __restrict__ m, const KCol
   const int k0 = iters[p];
   const int nrec = w.nrec[p] & ~kTrajEnded;
   const int max_iters = k0 + nrec - 1;
-  const int nwp = (nrec + kWin - 1) / kWin;
-  const T* ckp = w.ck + p * ck_per_problem(max_iters);
+  constexpr int K = kWinOf<T>;
+  const int wf = k0 / K, nwp = rec_windows<T>(max_iters);  // this problem's windows: wf .. nwp - 1 (absolute)
+  const T* ckp = w.ck + p * ck_per_problem<T>(max_iters);
   if (lane < npv) {
     const int pj = m->passive_q[lane];
     const T v = q_out[p * nq + pj];
@@ -1756,9 +1759,9 @@ __device__ inline void window_covers(const KModel<T>* __restrict__ m, const KCol
   }
   bool open[kCoverChunks];
 #pragma unroll
-  for (int k = 0; k < kCoverChunks; ++k) open[k] = lane + 64 * k < nwp;
+  for (int k = 0; k < kCoverChunks; ++k) open[k] = lane + 64 * k >= wf && lane + 64 * k < nwp;
   const bool boxes = w.box && nwp <= 64 * kCoverChunks;
-  for (int wt = 0, nc = 0; boxes && nc < kCoverCerts; ++nc) {  // wt: wave-uniform
+  for (int wt = wf, nc = 0; boxes && nc < kCoverCerts; ++nc) {  // wt: wave-uniform
     const T* ct = ckp + (int64_t)wt * kCkSlot;
     __syncthreads();  // RQ, BC, S.L free (the check, or the last round's tests, are done)
     if (lane < kRecPass)
@@ -1766,34 +1769,68 @@ __device__ inline void window_covers(const KModel<T>* __restrict__ m, const KCol
     else if (lane < kRecPassive)
       RQ[lane] = ct[kCkArm + kCkQ + lane - kRecPass];
     else if (lane < kRecPassive + npv)
-      RQ[lane] = k0 + wt * kWin > 0 ? PVc[lane - kRecPassive] : PVr[lane - kRecPassive];
+      RQ[lane] = max(k0, wt * K) > 0 ? PVc[lane - kRecPassive] : PVr[lane - kRecPassive];
     __syncthreads();
     scan_ball_cert(m, c, W.pair, RQ, SL, S.par, tgt, BC, S.L);
     const bool ok = BC.r > T(0);  // wave-uniform (LDS)
+    if (nc == 0) {  // the first passing iterate's certificate, as the resume kernel tests each iterate against it
+      T* tab = w.ctab + p * kCtab;
+      if (lane < 14) {
+        const int a = lane / 7, k = lane % 7;
+        const int slot = a == 0 ? k : (k == 0 ? -1 : kRecPass + k);
+        T qv = T(0), lv = T(0), in = T(0);
+        for (int e = 0; e < BC.n; ++e)
+          if (BC.off[e] == slot) {
+            qv = BC.qc[e];
+            lv = BC.lev[e];
+            in = T(1);
+          }
+        tab[a * kCkArm + kCtQc + k] = qv;
+        tab[a * kCkArm + kCtLev + k] = lv;
+        tab[a * kCkArm + kCtIn + k] = in;
+      } else if (lane == 14) {
+        T p0[2] = {T(0), T(0)}, p1[2] = {T(0), T(0)};  // passive joints at it = 0 (raw) and after (clamped)
+        for (int e = 0; e < BC.n; ++e)
+          if (BC.off[e] >= kRecPassive) {
+            const int pi = BC.off[e] - kRecPassive;
+            const T dr = fabs(PVr[pi] - BC.qc[e]), dc = fabs(PVc[pi] - BC.qc[e]);
+            p0[0] += dr;
+            p1[0] += dr * BC.lev[e];
+            p0[1] += dc;
+            p1[1] += dc * BC.lev[e];
+          }
+        tab[kCtR] = ok ? BC.r : T(-1);
+        tab[kCtPass] = p0[0];
+        tab[kCtPass + 1] = p1[0];
+        tab[kCtPass + 2] = p0[1];
+        tab[kCtPass + 3] = p1[1];
+      }
+    }
     int nxt = -1;
 #pragma unroll
     for (int k = 0; k < kCoverChunks; ++k) {
       const int wi = lane + 64 * k;
-      if (ok && open[k]) open[k] = !box_covers(BC, ckp + (int64_t)wi * kCkSlot, PVr, PVc, k0 + wi * kWin == 0);
+      if (ok && open[k]) open[k] = !box_covers(BC, ckp + (int64_t)wi * kCkSlot, PVr, PVc, max(k0, wi * K) == 0);
       const unsigned long long b = __ballot(open[k] && wi > wt);
       if (nxt < 0 && b) nxt = 64 * k + __ffsll((long long)b) - 1;
     }
     if (nxt < 0) break;
     wt = nxt;
   }
+  if (!boxes && lane == 0) w.ctab[p * kCtab + kCtR] = T(-1);  // no certificate: the resume kernel records every passing iterate
   bool any = false;
-  uint32_t* wm = w.wmask + p * mask_words(max_iters);
-  const int nmw = mask_words(max_iters);
+  uint32_t* wm = w.wmask + p * mask_words<T>(max_iters);
+  const int nmw = mask_words<T>(max_iters);
 #pragma unroll
   for (int k = 0; k < kCoverChunks; ++k) {
-    const unsigned long long b = __ballot(boxes ? open[k] : lane + 64 * k < nwp);
+    const unsigned long long b = __ballot(boxes ? open[k] : lane + 64 * k >= wf && lane + 64 * k < nwp);
     any = any || b != 0;
     if (lane < 2 && 2 * k + lane < nmw) wm[2 * k + lane] = (uint32_t)(b >> (32 * lane));
   }
   for (int k = 2 * kCoverChunks + lane; k < nmw; k += 64) wm[k] = ~0u;  // windows past the tested ones
   any = any || nmw > 2 * kCoverChunks;
   if (!any) {
-    const T* fr = ckp + (int64_t)rec_windows(max_iters) * kCkSlot;
+    const T* fr = ckp + ck_final<T>(max_iters);
     if (lane < nq) {
       const int rs = SL[lane];
       q_out[p * nq + lane] = rs < kRecPassive ? fr[rs] : PVc[rs - kRecPassive];
@@ -1898,10 +1935,13 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
 #endif
     // regenerated records (round 0 after round -2): only the windows the box
     // tests left (wm), the others proved colliding
-    const uint32_t* wm = w.wmask ? w.wmask + p * mask_words(it0 + nrec - 1) : nullptr;
-    int rstart = 0;
+    constexpr int K = kWinOf<T>;
+    const uint32_t* wm = w.wmask ? w.wmask + p * mask_words<T>(it0 + nrec - 1) : nullptr;
+    const uint64_t* rmw = w.rmask ? w.rmask + p * rec_windows<T>(it0 + nrec - 1) : nullptr;
+    int rstart = 0;  // record j is iterate it0 + j, in absolute window (it0 + j) / K
     if (wm)
-      while (rstart < nrec && !win_flagged(wm, rstart / kWin)) rstart += kWin;
+      for (int wa = it0 / K; rstart < nrec && !win_flagged(wm, wa); ++wa) rstart = (wa + 1) * K - it0;
+    rstart = min(rstart, nrec);
     if (w.by_p) {  // the batch kernels record no passive joints: constant from the first update on
       // staged in LDS first: read from q_out inside the loop, they were reloaded
       // after every record store (q_out may alias the records), a memory round
@@ -1915,7 +1955,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       }
       __syncthreads();
       for (int j = rstart + lane; j < nrec; j += 64)
-        if (!wm || win_flagged(wm, j / kWin))
+        if (!wm || (win_flagged(wm, (it0 + j) / K) && ((rmw[(it0 + j) / K] >> ((it0 + j) & (K - 1))) & 1ull)))
           for (int k = 0; k < npv; ++k) rec[(int64_t)j * RL + kRecPassive + k] = it0 + j > 0 ? S.cs[k] : S.sn[k];
       __syncthreads();
     }
@@ -1935,7 +1975,9 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       const unsigned long long cc0 = clock64();
 #endif
       const int j = start + lane;
-      const bool live = j < nrec && (!wm || win_flagged(wm, j / kWin));  // a record regenerated
+      // a record the resume kernel wrote: a window it regenerated, an iterate the certificate left
+      const bool live = j < nrec && (!wm || (win_flagged(wm, (it0 + j) / K) &&
+                                             ((rmw[(it0 + j) / K] >> ((it0 + j) & (K - 1))) & 1ull)));
       const T* r = rec + (int64_t)(live ? j : rstart) * RL;
       bool need = live && r[kRecPass] != T(0);
       // inscribed-ball certificates of the witness pair: every lane's motion
@@ -2038,8 +2080,8 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     const int a = ans >= 0 ? ans : (ended ? nrec - 1 : -1);
     if (a >= 0) {  // final: the answer, or the iterate after max_iters (success = False)
       // the latter from the batch kernel's final record when its window was not regenerated
-      const bool fin = ans < 0 && wm && !win_flagged(wm, a / kWin);
-      const T* r = fin ? w.ck + p * ck_per_problem(it0 + nrec - 1) + (int64_t)rec_windows(it0 + nrec - 1) * kCkSlot
+      const bool fin = ans < 0 && wm;
+      const T* r = fin ? w.ck + p * ck_per_problem<T>(it0 + nrec - 1) + ck_final<T>(it0 + nrec - 1)
                        : rec + (int64_t)a * RL;
       if (lane < nq) q_out[p * nq + lane] = (fin && SL[lane] >= kRecPassive) ? S.cs[SL[lane] - kRecPassive] : r[SL[lane]];
       if (lane < 2) err[p * 2 + lane] = sqrt(r[lane ? kRecErr1 : kRecErr0]);
@@ -2375,16 +2417,18 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
   };
   if (a.rec_used && *a.rec_used) {
     // the batch kernel wrote window checkpoints from each problem's first
-    // passing iterate (ikg_solve.hpp kWin): (1) one wave per problem of the
+    // passing iterate (ikg_solve.hpp kWinOf): (1) one wave per problem of the
     // batch checks it there and, when it collides, tests every window's box
     // against a certificate at that iterate (round -2); (2) the problems with
     // a window left are listed; (3) the batch kernel regenerates their
     // records from that window on (resume launch); (4) the records scan
     const size_t bi = ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255);
-    const size_t bm = ((sizeof(uint32_t) * (size_t)mask_words(prm.max_iters) * (size_t)a.B + 255) & ~(size_t)255);
+    const size_t bm = ((sizeof(uint32_t) * (size_t)mask_words<T>(prm.max_iters) * (size_t)a.B + 255) & ~(size_t)255);
     const size_t bc = ((sizeof(TrajCert<T>) * (size_t)a.B + 255) & ~(size_t)255);
+    const size_t bt = ((sizeof(T) * kCtab * (size_t)a.B + 255) & ~(size_t)255);
+    const size_t br = ((sizeof(uint64_t) * (size_t)rec_windows<T>(prm.max_iters) * (size_t)a.B + 255) & ~(size_t)255);
     char* dws = nullptr;
-    e = ws_alloc(a.ws_owner, (void**)&dws, bi + bm + bc, s);
+    e = ws_alloc(a.ws_owner, (void**)&dws, bi + bm + bc + bt + br, s);
     if (e != hipSuccess) return e;
     TrajWs<T> tw{};
     tw.rec = (T*)a.rec;
@@ -2393,13 +2437,18 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     tw.done = (int32_t*)dws;
     tw.wmask = (uint32_t*)(dws + bi);
     tw.cst = (TrajCert<T>*)(dws + bi + bm);
+    tw.ctab = (T*)(dws + bi + bm + bc);
+    uint64_t* rmask = (uint64_t*)(dws + bi + bm + bc + bt);
+    tw.rmask = rmask;
     tw.slots = a.B;
     tw.by_p = 1;
     tw.cert = scan_cert();
     tw.ck = (const T*)a.ck;
     tw.box = box_cover();
-    ws_trace("alloc scan", dws, bi + bm + bc, s);
+    ws_trace("alloc scan", dws, bi + bm + bc + bt + br, s);
     poison_int(dws, bi + bm + bc, s);
+    poison_float(tw.ctab, bt, s);
+    poison_int(rmask, br, s);
     // `done` is only written (read by later rounds, of which there are none here), so it needs no fill
     tw.wit_out = w.wit;
     if (first_fused(a.B)) {
@@ -2420,6 +2469,8 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     r.rec_list = w.clist;
     r.rec_count = w.count + 1;
     r.rec_wmask = tw.wmask;
+    r.rec_ctab = tw.ctab;
+    r.rec_rmask = rmask;
     ec = launch_pair_batch<T>(dm, prm, r, spec, s);
     if (ec == hipSuccess) {
       tw.wit_out = nullptr;

@@ -940,9 +940,14 @@ IKG_HD inline void deep_point_from(const Shape<float>& A, const Shape<float>& B,
   for (int i = 0; i < 3; ++i) D += (t[i] - s[i]) * (t[i] - s[i]);
   D = sqrtf(D);
   const float fm = D > 0.f ? fminf(fmaxf((D + ra - rb) / (2.f * D), 0.f), 1.f) : 0.5f;
+  // the candidates and the start's choice by selects, never a run-time index
+  // into a private array (that put the arrays in scratch memory: ~6.6 KB of
+  // scratch traffic per certificate wave)
   float best = -1e30f, base[4][3];
   int bi = 0;
+#pragma unroll
   for (int cnd = 0; cnd < 4; ++cnd) {
+#pragma unroll
     for (int i = 0; i < 3; ++i)
       base[cnd][i] = cnd == 0 ? s[i] + fm * (t[i] - s[i]) : cnd == 1 ? A.t[i] : cnd == 2 ? B.t[i]
                                                                        : 0.5f * (A.t[i] + B.t[i]);
@@ -952,15 +957,21 @@ IKG_HD inline void deep_point_from(const Shape<float>& A, const Shape<float>& B,
       bi = cnd;
     }
   }
+  const int b = start == 0 ? bi : start & 3;
   float x[3];
-  if (start == 0) {
-    for (int i = 0; i < 3; ++i) x[i] = base[bi][i];
-  } else {
-    const int b = start & 3, j = (start >> 2) % 3, side = (start / 12) & 1, sg = (start / 24) & 1;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) x[i] = b == 0 ? base[0][i] : b == 1 ? base[1][i] : b == 2 ? base[2][i] : base[3][i];
+  if (start != 0) {
+    const int j = (start >> 2) % 3, side = (start / 12) & 1, sg = (start / 24) & 1;
     const float mag = 0.5f * fmaxf(fminf(ra, rb), 1e-3f) * (1.f + (float)(start / 48));
-    const Shape<float>& S = side ? B : A;
-    for (int i = 0; i < 3; ++i) x[i] = base[b][i] + (sg ? -mag : mag) * (S.kind == kSphere ? (i == j ? 1.f : 0.f)
-                                                                                             : S.R[3 * i + j]);
+    const int kind = side ? B.kind : A.kind;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float ra0 = A.R[3 * i], ra1 = A.R[3 * i + 1], ra2 = A.R[3 * i + 2];
+      const float rb0 = B.R[3 * i], rb1 = B.R[3 * i + 1], rb2 = B.R[3 * i + 2];
+      const float axis = j == 0 ? (side ? rb0 : ra0) : j == 1 ? (side ? rb1 : ra1) : (side ? rb2 : ra2);
+      x[i] = x[i] + (sg ? -mag : mag) * (kind == kSphere ? (i == j ? 1.f : 0.f) : axis);
+    }
   }
   float scale = 0.f;
   for (int i = 0; i < 3; ++i) scale = fmaxf(scale, fmaxf(A.dims[i], B.dims[i]));

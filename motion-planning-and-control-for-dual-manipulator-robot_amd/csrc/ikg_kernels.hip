@@ -55,7 +55,9 @@ __global__ __launch_bounds__(64)
 #if IKG_WPE
 __attribute__((amdgpu_waves_per_eu(1, IKG_WPE)))
 #else
-__attribute__((amdgpu_waves_per_eu(kPairMinWaves<T, DAMPED, SP>)))
+// the resume kernel (REC = 2): few waves at most launches, so the registers of
+// one wave per SIMD (no spills)
+__attribute__((amdgpu_waves_per_eu(REC == 2 ? 1 : kPairMinWaves<T, DAMPED, SP>)))
 #endif
 void ikg_pair_batch_kernel(const KModel<T>* __restrict__ gm, KParams<T> prm,
                                                             const T* __restrict__ targets,
@@ -263,8 +265,10 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
       ra.list = a.rec_list;
       ra.count = a.rec_count;
       ra.wmask = a.rec_wmask;
+      ra.ctab = (const T*)a.rec_ctab;
+      ra.rmask = a.rec_rmask;
       // resume (a.rec_list): the same kernel over (listed problem, window) tasks, grid-stride
-      const dim3 g = a.rec_list ? dim3(resume_waves(a.B, rec_windows(prm.max_iters), ppw)) : grid;
+      const dim3 g = a.rec_list ? dim3(resume_waves(a.B, rec_windows<T>(prm.max_iters), ppw)) : grid;
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, g, dim3(64), lds_pad_bytes(), s, dmodel, prm, (const T*)a.targets,
                            (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out, a.converged, a.iters,

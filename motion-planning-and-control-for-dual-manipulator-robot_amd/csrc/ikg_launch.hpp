@@ -274,13 +274,15 @@ struct BatchArgs {
   // when the launch took them
   void* rec = nullptr;
   int32_t* rec_n = nullptr;
-  void* ck = nullptr;           // window checkpoints (ikg_solve.hpp kWin), ck_per_problem per problem
+  void* ck = nullptr;           // window checkpoints (ikg_solve.hpp kWinOf), ck_per_problem per problem
   bool* rec_used = nullptr;
   // resume launch (the collision scan's windows to regenerate, ikg_collision.hip):
   // listed problems, their count (device) and windows to regenerate per problem
   const int32_t* rec_list = nullptr;
   const int32_t* rec_count = nullptr;
   const uint32_t* rec_wmask = nullptr;
+  const void* rec_ctab = nullptr;   // per problem, the first check's certificate (ikg_solve.hpp kCtab)
+  uint64_t* rec_rmask = nullptr;    // per problem and window, the iterates the resume kernel recorded
   WsOwner* ws_owner = nullptr;  // scratch of captured solves (ws_alloc)
 };
 

@@ -32,7 +32,7 @@ namespace ikg {
 // the guarded step's LQ branch is an out-of-line call, and its spills and
 // stack frame are touched only when it is taken -- DESIGN.md §3a.5)
 // REC = 1: the collision continuation's window checkpoints (ikg_solve.hpp
-// kWin), written from the first passing iterate on, both arms' by the
+// kWinOf), written from the first passing iterate on, both arms' by the
 // problem's lane; the outputs at that iterate come from window 0's checkpoint
 // (solve_pair).  REC = 2, the resume launch: one lane per (listed problem,
 // window) task, grid-stride, restarting at the window's checkpoint and
@@ -53,29 +53,31 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
   // and spill the loop (with the guarded step's cold branch in the kernel)
   if constexpr (WPS == 2) asm volatile("" ::: "v171");
   if constexpr (REC == 2) {
-    const int nw = rec_windows(prm.max_iters);
+    constexpr int K = kWinOf<float>;
+    const int nw = rec_windows<float>(prm.max_iters);
     const int64_t ntask = (int64_t)(*ra.count) * nw;
     const int rl = rec_len(m->n_passive);
     for (int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x; t < ntask; t += (int64_t)gridDim.x * 64) {
       const int64_t i = t / nw;
       const int w = (int)(t - i * nw);
       const int64_t p = ra.list[i];
-      const int nr = ra.nrec[p] & ~kTrajEnded;
-      if (w * kWin >= nr || !win_flagged(ra.wmask + p * mask_words(prm.max_iters), w)) continue;
       const int k0 = iters_out[p];
+      if (w < k0 / K || !win_flagged(ra.wmask + p * mask_words<float>(prm.max_iters), w)) continue;
       const int64_t tgt = S > 1 ? p / S : p;
       const int64_t row = S > 1 ? p - tgt * S : p;
       v2f RT[9], tT[3];
       hook_target_packed(m, targets + tgt * 12, RT, tT);
-      float* ckw = ra.ck + p * ck_per_problem(prm.max_iters) + (int64_t)w * kCkSlot;
+      float* ckw = ra.ck + p * ck_per_problem<float>(prm.max_iters) + (int64_t)w * kCkSlot;
       v2f qc = v2f{ckw[kCkQ], ckw[kCkArm + kCkQ]}, qa[kArmDof];
 #pragma unroll
       for (int k = 0; k < kArmDof; ++k) qa[k] = v2f{ckw[kCkQ + 1 + k], ckw[kCkArm + kCkQ + 1 + k]};
       RecOut<float> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
                        q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl, ckw};
+      ro.ctab = ra.ctab + p * kCtab;
+      ro.rmask = ra.rmask + p * nw + w;
       ro.k0 = k0;
-      ro.it_start = k0 + w * kWin;
-      ro.it_stop = k0 + min((w + 1) * kWin, nr);
+      ro.it_start = max(k0, w * K);
+      ro.it_stop = min((w + 1) * K, prm.max_iters + 1);
       int it;
       bool conv;
       v2f nrm, other;
@@ -100,7 +102,7 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
     const int rl = rec_len(m->n_passive);
     RecOut<float> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, qrow,
                      q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl,
-                     ra.ck + p * ck_per_problem(prm.max_iters)};
+                     ra.ck + p * ck_per_problem<float>(prm.max_iters)};
     ra.nrec[p] = 0;
     if (solve_pair<v2f, false, SP, MED, 1>(m, prm, 0, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
@@ -183,8 +185,10 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
   ra.list = a.rec_list;
   ra.count = a.rec_count;
   ra.wmask = a.rec_wmask;
+  ra.ctab = (const float*)a.rec_ctab;
+  ra.rmask = a.rec_rmask;
   // resume (a.rec_list): the instantiation the batch launch took (need from a.B), grid-stride over tasks
-  const dim3 g = a.rec_list ? dim3(resume_waves(a.B, rec_windows(prm.max_iters), 64)) : grid;
+  const dim3 g = a.rec_list ? dim3(resume_waves(a.B, rec_windows<float>(prm.max_iters), 64)) : grid;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, g, dim3(64), packed_lds_pad(), s, dmodel, prm, (const float*)a.targets,
                        (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out, a.converged, a.iters,

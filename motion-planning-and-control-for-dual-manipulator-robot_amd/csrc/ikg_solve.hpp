@@ -93,31 +93,57 @@ __device__ __forceinline__ void store_block4(T* dst, const T (&v)[4]) {
 
 // ---- window checkpoints (round 6: the records' window form)
 // The batch kernel no longer writes every iterate past the first passing one
-// (k0): it writes, every kWin iterates from k0 on, a checkpoint of the loop's
-// whole state (q, the carried trig and rotation-angle values) and the window's
-// path length L (the sum over its updates of the largest joint step), and at
-// the end the record of the iterate after max_iters.  Every iterate of window
-// w lies within L_w of the window's first iterate in every joint, so the scan
-// proves a whole window colliding with one certificate test on that box
-// (ikg_collision.hip round -3); a window the box test does not prove is
-// regenerated from its checkpoint by the same kernel (RecArgs::list, "resume"),
-// bit for bit the iterates the batch loop ran, into the records the scan reads.
-// Slot layout per problem: (rec_windows + 1) slots of kCkSlot values; window w
-// in slot w, the final record (record layout, passive joints not filled) in
-// the last.  Within a slot, per arm (pair layout: the arm's lane; packed: the
-// arm's half) at arm * kCkArm:
-//   [0, 8)   root, the arm's joints, |e|^2   (the record block layout)
-//   [8, 15)  sn[0..6]      [16, 23) cs[0..6]
-//   [24, 27) rotation-angle track (fp64 pair layout)   [28] L
-constexpr int kWin = 32;  // iterates per window
+// (k0).  Windows are aligned to absolute update counts (window w: iterates
+// [w K, (w + 1) K), K = 32); from k0 on it writes a checkpoint at k0 (the
+// loop's whole state: q, the carried trig, the rotation-angle track) and at
+// each later window's first iterate (q and the previous window's path length
+// L: the sum over its updates of the largest joint step), and at the end the
+// record of the iterate after max_iters.  In the record-writing kernels the
+// carried trig and angle are recomputed exactly every kRsRec updates, so at a
+// window start they are a function of q (fp32 resyncs every 16 anyway; fp64
+// every 32 there instead of 128: ~2% more work in that kernel).  Every iterate
+// of window w lies within L_w of the window's first one in every joint, so the
+// scan proves a whole window colliding with one certificate test on that box
+// (ikg_collision.hip round -2); a window the box test does not prove is
+// regenerated from its checkpoint (the resume kernel, RecArgs::list) into the
+// records the scan reads.
+// Slot layout per problem: rec_windows + 2 slots of kCkSlot values; window w in
+// slot w (absolute); the final record (record layout, passive joints not
+// filled) in the last.  Within a slot, per arm (pair layout: the arm's lane;
+// packed: the arm's half) at arm * kCkArm:
+//   k0's window:   [0, 8) root, the arm's joints, |e|^2 (the record block
+//                  layout); [8, 15) sn; [16, 23) cs; [24, 27) angle track
+//   later windows: [0, 8) root, the arm's joints, L of window w - 1
+// (the last window's length goes to the next slot, before the final record's)
+constexpr int kWin = 32;  // iterates per window (a power of 2, at most 64: one 64-bit record mask per window)
 constexpr int kCkArm = 32, kCkSlot = 64;
-constexpr int kCkQ = 0, kCkSn = 8, kCkCs = 16, kCkTk = 24, kCkL = 28;
-IKG_HD inline int rec_windows(int max_iters) { return (max_iters + 1 + kWin - 1) / kWin; }
-IKG_HD inline int64_t ck_per_problem(int max_iters) { return (int64_t)(rec_windows(max_iters) + 1) * kCkSlot; }
+constexpr int kCkQ = 0, kCkSn = 8, kCkCs = 16, kCkTk = 24, kCkL = 7;
+template <typename E>
+constexpr int kWinOf = kWin;
+template <typename T>
+constexpr int kRsRec = Trig<T>::kResync < kWin ? Trig<T>::kResync : kWin;  // divides kWin
+template <typename E>
+IKG_HD inline int rec_windows(int max_iters) { return max_iters / kWinOf<E> + 1; }
+template <typename E>
+IKG_HD inline int64_t ck_per_problem(int max_iters) { return (int64_t)(rec_windows<E>(max_iters) + 2) * kCkSlot; }
+template <typename E>
+IKG_HD inline int64_t ck_final(int max_iters) { return (int64_t)(rec_windows<E>(max_iters) + 1) * kCkSlot; }
 // the windows the scan could not prove colliding (regenerated and scanned):
 // one bit per window, mask_words 32-bit words per problem
-IKG_HD inline int mask_words(int max_iters) { return (rec_windows(max_iters) + 31) / 32; }
+template <typename E>
+IKG_HD inline int mask_words(int max_iters) { return (rec_windows<E>(max_iters) + 31) / 32; }
 IKG_HD inline bool win_flagged(const uint32_t* wm, int w) { return (wm[w >> 5] >> (w & 31)) & 1u; }
+
+// The first check's certificate as the resume kernel reads it (written by
+// ikg_collision.hip window_covers for a listed problem): per arm at
+// arm * kCkArm (the pair layout's lane; the packed layout's half) its 7
+// joints -- root (arm 0 only) and the arm's -- with the certified value, the
+// lever arm and whether the joint is on a chain the certificate bounds; the
+// radius (<= 0: none); the passive joints' fixed contribution, for an iterate
+// at it = 0 (raw) and after (clamped).  Each iterate's motion bound is then
+// ball_covers' over both sides together (the sum of both geometries' terms:
+// sound, slightly weaker than per side).
+constexpr int kCtQc = 0, kCtLev = 8, kCtIn = 16, kCtR = 64, kCtPass = 65, kCtab = 72;
 
 // Kernel argument of the record-writing (REC) batch kernels.
 template <typename T>
@@ -128,6 +154,8 @@ struct RecArgs {
   const int32_t* list = nullptr;    // resume launch: the problems whose windows are regenerated (null: the batch solve)
   const int32_t* count = nullptr;   // resume: list length (device)
   const uint32_t* wmask = nullptr;  // resume: per problem, the windows to regenerate (mask_words each)
+  const T* ctab = nullptr;          // resume: per problem, the first check's certificate (kCtab values)
+  uint64_t* rmask = nullptr;        // resume: per problem and window, the iterates recorded (rec_windows each)
 };
 
 // Record-in-batch outputs of one problem (the REC batch kernels): the loop goes
@@ -146,6 +174,8 @@ struct RecOut {
   int rl;               // rec_len
   T* ck;                // its checkpoint slots (resume: the window's)
   int it_start = 0, k0 = -1, it_stop = 0;  // resume: first iterate, the problem's k0, one past the last iterate
+  const T* ctab = nullptr;    // resume: its certificate table
+  uint64_t* rmask = nullptr;  // resume: this window's recorded iterates (bit j - first)
 };
 
 // Diagnostic build only (-DIKG_STAGE_CLOCK, tools/stage_clock.py; no stamp
@@ -224,6 +254,35 @@ __device__ __forceinline__ void ck_put(typename LaneT<T>::E* c, int arm, int off
   }
 }
 
+template <typename T>
+__device__ __forceinline__ bool resume_covered(const typename LaneT<T>::E* __restrict__ tab, int arm, T qc,
+                                               const T* qa, int it) {
+  using E = typename LaneT<T>::E;
+  const E r = tab[kCtR];
+  T s0 = T(0), s1 = T(0);
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const T v = k == 0 ? qc : qa[k - 1];
+    const T qcv = ck_get<T>(tab, arm, kCtQc + k), lev = ck_get<T>(tab, arm, kCtLev + k),
+            in = ck_get<T>(tab, arm, kCtIn + k);
+    const T dd = fabs(v - qcv) * in;
+    s0 = s0 + dd;
+    s1 = s1 + dd * lev;
+  }
+  E a0, a1;
+  if constexpr (is_packed<T>) {
+    a0 = s0.x + s0.y;
+    a1 = s1.x + s1.y;
+  } else {
+    a0 = s0 + pair_swap(s0);
+    a1 = s1 + pair_swap(s1);
+  }
+  const int pc = it > 0 ? 2 : 0;
+  a0 += tab[kCtPass + pc];
+  a1 += tab[kCtPass + pc + 1];
+  return r > E(0) && a1 + r * a0 < r;
+}
+
 // REC = 1: from the first passing iterate on, the window checkpoints go into
 // this problem's fixed slots (ikg_capi.hip sizes the launches so the slots fit
 // the record budget: no shared state, so a problem's checkpoints and answer do
@@ -251,19 +310,24 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   int it = 0;
   ThetaTrack<T> tk{};
   T L = T(0);  // REC: this window's path length (largest joint step per update, summed)
+  uint64_t rbits = 0;  // REC = 2: the window's recorded iterates
   if constexpr (REC == 2) {  // the loop state at the checkpoint (qc, qa: the caller, from the same slot)
-#pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      sn[j] = ck_get<T>(ro->ck, arm, kCkSn + j);
-      cs[j] = ck_get<T>(ro->ck, arm, kCkCs + j);
-    }
-    if constexpr (!is_packed<T>) {
-      tk.th = ck_get<T>(ro->ck, arm, kCkTk);
-      tk.st = ck_get<T>(ro->ck, arm, kCkTk + 1);
-      tk.ct = ck_get<T>(ro->ck, arm, kCkTk + 2);
-    }
     it = ro->it_start;
     k0 = ro->k0;
+    if (it == k0) {
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        sn[j] = ck_get<T>(ro->ck, arm, kCkSn + j);
+        cs[j] = ck_get<T>(ro->ck, arm, kCkCs + j);
+      }
+      if constexpr (!is_packed<T>) {
+        tk.th = ck_get<T>(ro->ck, arm, kCkTk);
+        tk.st = ck_get<T>(ro->ck, arm, kCkTk + 1);
+        tk.ct = ck_get<T>(ro->ck, arm, kCkTk + 2);
+      }
+    } else {  // a window start after k0: the trig resynced exactly there (kRsRec), the angle track is recomputed
+      trig_exact_f1(m, arm, qc, qa, sn, cs);
+    }
   } else if constexpr (F1) {
     trig_exact_f1(m, arm, qc, qa, sn, cs);
   } else {
@@ -304,7 +368,9 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 #endif
     // fp32: atan2f is as cheap as the tracked angle (measured)
     ThetaTrack<T>* tkp = (IKG_THETA_TRACK && is_f64<T>) ? &tk : nullptr;
-    const bool resync = (it % Trig<T>::kResync) == 0;
+    // the record-writing kernels resync at every window start (kRsRec)
+    constexpr int kRs = REC ? kRsRec<T> : Trig<T>::kResync;
+    const bool resync = (it % kRs) == 0;
     // the step is formed before the stop test (discarded when the loop ends)
     // so the test's exchange/compare overlaps the solve instead of heading it
     T dq[6], alpha, beta, s;
@@ -368,40 +434,50 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
         }
       };
       if (k0 >= 0) {
+        constexpr int K = kWinOf<E>;
         const int j = it - k0;
-        if constexpr (REC == 2) {  // a regenerated window: every iterate's record
-          put_record(recp + (int64_t)j * ro->rl);
+        if constexpr (REC == 2) {  // a regenerated window: the passing iterates the certificate does not prove
+          if (pass && !resume_covered<T>(ro->ctab, arm, qc, qa, it)) {
+            put_record(recp + (int64_t)j * ro->rl);
+            rbits |= 1ull << (it & (K - 1));
+          }
           if (it + 1 >= ro->it_stop) break;
         } else {
-          if (j % kWin == 0) {  // a window starts: the previous one's length, then this state
-            E* cw = ro->ck + (int64_t)(j / kWin) * kCkSlot;
+          // a window starts (absolute iterate counts: wave-uniform), or this
+          // problem's first passing iterate: its state, and the previous
+          // window's length (slot w holds L_{w-1}, written with the state so
+          // each slot goes out as whole lines)
+          const bool wstart = (it & (K - 1)) == 0;
+          if (wstart || j == 0) {
+            E* cw = ro->ck + (int64_t)(it / K) * kCkSlot;
             const T z = T(0);
-            if (j > 0) {
-              const T lv[4] = {L, z, z, z};
-              ck_put<T, 4>(cw - kCkSlot, arm, kCkL, lv);
-            }
             T qb[8];
             qb[0] = qc;
 #pragma unroll
             for (int k = 0; k < kArmDof; ++k) qb[1 + k] = qa[k];
-            qb[7] = x;
+            qb[7] = j == 0 ? x : L;  // k0's window: its error (the outputs); later: the last window's length
             ck_put<T, 8>(cw, arm, kCkQ, qb);
-            const T sb[8] = {sn[0], sn[1], sn[2], sn[3], sn[4], sn[5], sn[6], z};
-            const T cb[8] = {cs[0], cs[1], cs[2], cs[3], cs[4], cs[5], cs[6], z};
-            ck_put<T, 8>(cw, arm, kCkSn, sb);
-            ck_put<T, 8>(cw, arm, kCkCs, cb);
-            if constexpr (!is_packed<T>) {
-              const T tb[4] = {tk.th, tk.st, tk.ct, z};
-              ck_put<T, 4>(cw, arm, kCkTk, tb);
+            if (j == 0) {  // k0's state (later window starts: a function of q, kRsRec)
+              const T sb[8] = {sn[0], sn[1], sn[2], sn[3], sn[4], sn[5], sn[6], z};
+              const T cb[8] = {cs[0], cs[1], cs[2], cs[3], cs[4], cs[5], cs[6], z};
+              ck_put<T, 8>(cw, arm, kCkSn, sb);
+              ck_put<T, 8>(cw, arm, kCkCs, cb);
+              if constexpr (!is_packed<T>) {
+                const T tb[4] = {tk.th, tk.st, tk.ct, z};
+                ck_put<T, 4>(cw, arm, kCkTk, tb);
+              }
             }
             L = z;
           }
-          if (ended) {  // the last window's length, and the iterate after max_iters as a record
-            E* cw = ro->ck + (int64_t)(j / kWin) * kCkSlot;
-            const T z = T(0);
-            const T lv[4] = {L, z, z, z};
-            ck_put<T, 4>(cw, arm, kCkL, lv);
-            put_record(ro->ck + (int64_t)rec_windows(prm.max_iters) * kCkSlot);
+          if (ended) {  // the last window's length (in the next slot), and the iterate after max_iters as a record
+            E* cw = ro->ck + (int64_t)(it / K + 1) * kCkSlot;
+            if constexpr (is_packed<T>) {
+              cw[kCkL] = L.x;
+              cw[kCkArm + kCkL] = L.y;
+            } else {
+              cw[arm * kCkArm + kCkL] = L;
+            }
+            put_record(ro->ck + ck_final<E>(prm.max_iters));
           }
         }
       }
@@ -434,7 +510,7 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     sc_acc[3] += sc_t0 - sc_t1;
 #endif
     if constexpr (F1) {
-      trig_advance_f1<T, MED>(m, arm, qc, qa, q_old, (it % Trig<T>::kResync) == 0, sn, cs);
+      trig_advance_f1<T, MED>(m, arm, qc, qa, q_old, (it % (REC ? kRsRec<T> : Trig<T>::kResync)) == 0, sn, cs);
 #ifdef IKG_STAGE_CLOCK
       IKG_STAMP(sc_t1);
       sc_acc[4] += sc_t1 - sc_t0;
@@ -461,15 +537,19 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
   if (any_of(ps == T(-12345.678))) it = -1;  // never true; keeps the padding live
 #endif
   if constexpr (REC) {
-    if constexpr (REC == 2) return true;  // records only: the scan writes the outputs
+    if constexpr (REC == 2) {  // records only: the scan writes the outputs
+      if (is_packed<T> || arm == 0) *ro->rmask = rbits;
+      return true;
+    }
     if (k0 >= 0) {
       // the outputs at the first passing iterate, from window 0's checkpoint
       // (this lane's own q block): writing them inside the loop put a
       // divergent branch into every update (records-in-batch kernel 4% slower)
+      const E* c0 = ro->ck + (int64_t)(k0 / kWinOf<E>) * kCkSlot;  // the slot of k0's window
       if constexpr (is_packed<T>) {
         float b[2][8], qa0[kArmDof];
-        load_block8(ro->ck + kCkQ, b[0]);
-        load_block8(ro->ck + kCkArm + kCkQ, b[1]);
+        load_block8(c0 + kCkQ, b[0]);
+        load_block8(c0 + kCkArm + kCkQ, b[1]);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -482,7 +562,7 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
         *ro->nrec = (it - k0 + 1) | kTrajEnded;
       } else {
       T blk[8];
-      load_block8(ro->ck + arm * kCkArm + kCkQ, blk);
+      load_block8(c0 + arm * kCkArm + kCkQ, blk);
       T qa0[kArmDof];
 #pragma unroll
       for (int k = 0; k < kArmDof; ++k) qa0[k] = blk[1 + k];
@@ -520,19 +600,19 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
   const int lane = threadIdx.x;
   const int arm = lane & 1;
   if constexpr (REC == 2) {
-    const int nw = rec_windows(prm.max_iters);
+    constexpr int K = kWinOf<T>;
+    const int nw = rec_windows<T>(prm.max_iters);
     const int64_t ntask = (int64_t)(*ra.count) * nw;
     const int rl = rec_len(m->n_passive);
-    const int64_t ckpp = ck_per_problem(prm.max_iters);
+    const int64_t ckpp = ck_per_problem<T>(prm.max_iters);
     for (int64_t t0 = (int64_t)blockIdx.x * ppw; t0 < ntask; t0 += (int64_t)gridDim.x * ppw) {
       const int64_t t = t0 + (lane >> 1);
       if (lane >= 2 * ppw || t >= ntask) continue;  // both lanes of a pair together
       const int64_t i = t / nw;
       const int w = (int)(t - i * nw);
       const int64_t p = ra.list[i];
-      const int nr = ra.nrec[p] & ~kTrajEnded;
-      if (w * kWin >= nr || !win_flagged(ra.wmask + p * mask_words(prm.max_iters), w)) continue;
       const int k0 = iters_out[p];
+      if (w < k0 / K || !win_flagged(ra.wmask + p * mask_words<T>(prm.max_iters), w)) continue;
       const int64_t tgt = S > 1 ? p / S : p;
       const int64_t row = S > 1 ? p - tgt * S : p;
       T RT[9], tT[3];
@@ -544,9 +624,11 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
       for (int k = 0; k < kArmDof; ++k) qa[k] = cq[1 + k];
       RecOut<T> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
                    q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl, ckw};
+      ro.ctab = ra.ctab + p * kCtab;
+      ro.rmask = ra.rmask + p * nw + w;
       ro.k0 = k0;
-      ro.it_start = k0 + w * kWin;
-      ro.it_stop = k0 + min((w + 1) * kWin, nr);
+      ro.it_start = max(k0, w * K);
+      ro.it_stop = min((w + 1) * K, prm.max_iters + 1);
       int it;
       bool conv;
       T nrm, other;
@@ -570,7 +652,7 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
   if constexpr (REC == 1) {  // the continuation's checkpoints (ikg_collision.hip): outputs at the first passing iterate
     const int rl = rec_len(m->n_passive);
     RecOut<T> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, qrow, q_out + p * m->nq,
-                 conv_out + p, iters_out + p, err_out + p * 2, rl, ra.ck + p * ck_per_problem(prm.max_iters)};
+                 conv_out + p, iters_out + p, err_out + p * 2, rl, ra.ck + p * ck_per_problem<T>(prm.max_iters)};
     if (arm == 0) ra.nrec[p] = 0;
     if (solve_pair<T, DAMPED, SP, MED, 1>(m, prm, arm, RT, tT, qc, qa, it, conv, nrm, other, &ro)) return;
   } else {
