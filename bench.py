@@ -329,27 +329,35 @@ def iters_hist(iters, max_iters=1000, width=50):
     return h
 
 
-REC_BUDGET_MB = 24576  # ikg_capi.hip kRecBudgetMB (IKG_REC_BUDGET_MB overrides)
+REC_BUDGET_MB, CK_BUDGET_MB = 1024, 16384  # ikg_capi.hip kRecBudgetMB / kCkBudgetMB (IKG_REC_BUDGET_MB / IKG_CK_BUDGET_MB)
 
 
 def collision_kernels(kname, dtype, B, S=0):
     """The kernels a collision solve runs, by the C-ABI's rules
-    (ikg_capi.hip rec_chunk, ikg_collision.hip launch_collide_continue): the
-    batch kernel writing window checkpoints, in launches whose fixed slots fit
-    the budget, then per launch the first check with the window-box tests
-    (ikg_traj_scan_kernel round -2), the compaction, the resume launch of the
-    batch kernel (windows left to regenerate) and the records scan."""
+    (ikg_capi.hip rec_chunk / offer_records, ikg_collision.hip
+    launch_collide_continue): the batch kernel writing window checkpoints, in
+    launches whose checkpoints fit their budget; then per launch the first
+    check with the window-box tests (ikg_traj_scan_kernel round -2: fused up to
+    65,536 problems, else the pre-screen and the boxes over its list), the
+    compaction, and per records round the resume launch of the batch kernel
+    (windows left) and the records scan."""
     esz = 8 if dtype == "f64" else 4
-    slot = esz * (20 * 1001 + 64 * 33) * max(S, 1)  # one unit's records + checkpoints (a target's S seeds)
-    budget = int(os.environ.get("IKG_REC_BUDGET_MB", str(REC_BUDGET_MB))) << 20
-    cap = max(1, budget // slot)
+    ck = esz * 64 * (1000 // 32 + 3) * max(S, 1)  # one unit's checkpoints (a target's S seeds)
+    rec = esz * 20 * 1001  # one listed problem's records
+    budget = int(os.environ.get("IKG_CK_BUDGET_MB", str(CK_BUDGET_MB))) << 20
+    cap = max(1, budget // ck)
     chunks = 1 if B <= cap else -(-B // cap)
     per = -(-B // chunks) * max(S, 1)  # problems per launch
-    label = (kname + " (window checkpoints past the first passing iterate) + ikg_traj_scan_kernel (first check"
-             " and window boxes) + ikg_compact_count_kernel + ikg_compact_write_kernel + " + kname +
-             " (resume: windows left) + ikg_traj_scan_kernel (records scan)")
+    slots = max(1, (int(os.environ.get("IKG_REC_BUDGET_MB", str(REC_BUDGET_MB))) << 20) // rec)
+    rounds = -(-per // min(per, slots))
+    fused = per <= 65536 if "IKG_PRESCAN" not in os.environ else os.environ["IKG_PRESCAN"] != "0"
+    label = (kname + " (window checkpoints past the first passing iterate) + " +
+             ("ikg_first_check_kernel (first check and window boxes)" if fused else
+              "ikg_prescreen_kernel + compaction + ikg_first_check_kernel (window boxes over its list)") +
+             " + ikg_compact_count_kernel + ikg_compact_write_kernel + " + kname +
+             f" (resume: windows left) + ikg_traj_scan_kernel (records scan), {rounds} records round(s)")
     if chunks > 1:
-        label += f"; {chunks} launch sequences of {per} problems (records budget {budget >> 20} MB)"
+        label += f"; {chunks} launch sequences of {per} problems (checkpoint budget {budget >> 20} MB)"
     return label, "the whole solve (all its kernels)"
 
 

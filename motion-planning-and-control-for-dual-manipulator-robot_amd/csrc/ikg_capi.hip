@@ -232,26 +232,29 @@ static bool rec_in_batch() {
   const char* e = getenv("IKG_TRAJ_REC");
   return !(e && atoi(e) == 0);
 }
-// Budget 24 GiB (~8% of an MI355X's 288 GB, held only while a collision solve
-// runs: the model's scratch pool keeps 1.25 GiB between solves, ikg_launch.hpp
-// ws_keep_bytes): the records of one launch, (max_iters + 1) per problem in
-// fixed slots (C2 fp64: 656 MB; C3 fp32: 5.2 GB; C5's 131,072 fp32 problems:
-// 10.5 GB; C4's 131,072-problem fp64 share: 21 GB).  A batch whose records
-// exceed it is solved in chunks of equal size that fit (C4 on one GPU, fp64:
-// 7 chunks), one launch sequence per chunk on the stream.  Fixed slots carry
-// no shared state, so a problem's answer does not depend on the chunking or on
-// the order its launch's waves run in.  (Round 5 handed out records from one
-// pool by a per-problem atomic instead; when it ran dry, which problems fell
-// back to the record-free continuation depended on wave scheduling, and that
-// path agrees with the records only to rounding -- VERDICT r5)
-// Measured against round 5's pool (profiles/r06/records/): C2 and C3 + collision
-// unchanged; C4 share fp64 + collision 6.44 ms pooled, 6.43 in one launch at
-// 24 GiB, 6.67 in two at 12 GiB, 10.0 in four at 6 GiB; C5 + collision 3.58 ms
-// pooled, 3.72 in fixed slots.  IKG_REC_BUDGET_MB overrides.
-constexpr size_t kRecBudgetMB = 24576;
+// Memory of a collision solve (round 6, window checkpoints, ikg_solve.hpp):
+//  * checkpoints, one area per problem of a launch (ck_per_problem: 34 slots,
+//    17 KB in fp64, 8.7 KB in fp32 at max_iters 1,000: C2 71 MB, C3 570 MB,
+//    C4's 131,072-problem fp64 share 2.3 GB).  A batch whose checkpoints exceed
+//    the checkpoint budget (16 GiB, IKG_CK_BUDGET_MB) is solved in chunks of
+//    equal size that fit, one launch sequence per chunk (fixed slots carry no
+//    shared state, so a problem's answer does not depend on the chunking);
+//  * the regenerated records of the problems the scan lists, (max_iters + 1)
+//    records per problem, for as many problems as the records budget holds
+//    (1 GiB, IKG_REC_BUDGET_MB: 6,700 fp64 / 13,400 fp32 problems); the resume
+//    kernel and the records scan run in rounds of that many list entries
+//    (ikg_collision.hip launch_collide_continue).
+// Round 5 held every problem's records (C3 fp32 5.2 GB, the C4 share 21 GB)
+// under a 24 GiB budget; the model's pool keeps 1.25 GiB between solves
+// (ikg_launch.hpp ws_keep_bytes).
+constexpr size_t kRecBudgetMB = 1024, kCkBudgetMB = 16384;
 static size_t rec_budget() {
-  if (const char* e = getenv("IKG_REC_BUDGET_MB")) return (size_t)atoll(e) << 20;
+  if (const char* e = getenv("IKG_REC_BUDGET_MB")) return std::max<size_t>(1, (size_t)atoll(e)) << 20;
   return kRecBudgetMB << 20;
+}
+static size_t ck_budget() {
+  if (const char* e = getenv("IKG_CK_BUDGET_MB")) return std::max<size_t>(1, (size_t)atoll(e)) << 20;
+  return kCkBudgetMB << 20;
 }
 
 // the final record (record layout) fits a checkpoint slot (ikg_solve.hpp kCkSlot)
@@ -259,38 +262,39 @@ static bool rec_fits(int nq) {
   return ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof)) <= ikg::kCkSlot;
 }
 
-// bytes of one problem's record slot (the regenerated records) and window
-// checkpoints (ikg_solve.hpp kWinOf)
+// bytes of one problem's regenerated records, and of its checkpoints
 template <typename T>
 static size_t rec_records_bytes(const ikg_params& params, int nq) {
   const size_t rl = (size_t)ikg::rec_len(std::max(0, nq - 1 - 2 * ikg::kArmDof));
   return sizeof(T) * rl * ((size_t)params.max_iters + 1);
 }
 template <typename T>
-static size_t rec_slot_bytes(const ikg_params& params, int nq) {
-  return rec_records_bytes<T>(params, nq) + sizeof(T) * (size_t)ikg::ck_per_problem<T>(params.max_iters);
+static size_t rec_ck_bytes(const ikg_params& params) {
+  return sizeof(T) * (size_t)ikg::ck_per_problem<T>(params.max_iters);
 }
 
 // units (problems, or multi-start targets of `per_unit` problems each) per
-// launch: all of them when their records fit the budget, else the fewest equal
-// chunks that do (at least one unit)
+// launch: all of them when their checkpoints fit the budget, else the fewest
+// equal chunks that do (at least one unit)
 template <typename T>
-static int64_t rec_chunk(const ikg_params& params, int nq, int64_t units, int64_t per_unit) {
-  const size_t unit_bytes = rec_slot_bytes<T>(params, nq) * (size_t)per_unit;
-  const int64_t cap = std::max<int64_t>(1, (int64_t)(rec_budget() / std::max<size_t>(1, unit_bytes)));
+static int64_t rec_chunk(const ikg_params& params, int64_t units, int64_t per_unit) {
+  const size_t unit_bytes = rec_ck_bytes<T>(params) * (size_t)per_unit;
+  const int64_t cap = std::max<int64_t>(1, (int64_t)(ck_budget() / std::max<size_t>(1, unit_bytes)));
   if (units <= cap) return units;
   const int64_t n = (units + cap - 1) / cap;
   return (units + n - 1) / n;
 }
 
-// Records of the collision continuation for `n` problems (one chunk, see
-// solve_batch_t): fixed slots of (max_iters + 1) records.  Null when the
-// allocation fails (the continuation then runs without records).
+// Checkpoints and records of the collision continuation for `n` problems (one
+// chunk, see solve_batch_t): checkpoints for all n, records for the records
+// budget's capacity (a.rec_slots).  Null when the allocation fails (the
+// continuation then runs without them).
 template <typename T>
 void* offer_records(ikg_model* model, ikg::BatchArgs& a, const ikg_params& params, int64_t n, int nq, hipStream_t s,
                     bool* rec_used) {
-  const size_t b_rec = (rec_records_bytes<T>(params, nq) * (size_t)n + 255) & ~(size_t)255;
-  const size_t b_ck = (sizeof(T) * (size_t)ikg::ck_per_problem<T>(params.max_iters) * (size_t)n + 255) & ~(size_t)255;
+  const int64_t slots = std::min<int64_t>(n, std::max<int64_t>(1, (int64_t)(rec_budget() / rec_records_bytes<T>(params, nq))));
+  const size_t b_rec = (rec_records_bytes<T>(params, nq) * (size_t)slots + 255) & ~(size_t)255;
+  const size_t b_ck = (rec_ck_bytes<T>(params) * (size_t)n + 255) & ~(size_t)255;
   const size_t b_n = (sizeof(int32_t) * (size_t)n + 255) & ~(size_t)255;
   void* rec = nullptr;
   if (ikg::ws_alloc(&model->ws, &rec, b_rec + b_ck + b_n, s) != hipSuccess) {
@@ -300,6 +304,7 @@ void* offer_records(ikg_model* model, ikg::BatchArgs& a, const ikg_params& param
   a.rec = rec;
   a.ck = (char*)rec + b_rec;
   a.rec_n = (int32_t*)((char*)rec + b_rec + b_ck);
+  a.rec_slots = slots;
   ikg::ws_trace("alloc rec", rec, b_rec + b_ck + b_n, s);
   ikg::poison_float(rec, b_rec + b_ck, s);
   ikg::poison_int(a.rec_n, sizeof(int32_t) * (size_t)n, s);
@@ -372,7 +377,7 @@ int solve_batch_t(ikg_model* model, int device, const void* targets, const void*
   const ikg::KParams<T> kp = kparams<T>(params);
   if (dc && model->spec == ikg::kSpecNextage && !(params->lambda > 0) && !a.jit && rec_in_batch() &&
       rec_fits(nq) && ikg::resolve_variant<T>(kp, model->spec, a.variant, B, true) != IKG_VARIANT_QUAD) {
-    chunk = rec_chunk<T>(*params, nq, B, 1);
+    chunk = rec_chunk<T>(*params, B, 1);
     rec = offer_records<T>(model, a, *params, chunk, nq, s, &rec_used);
     if (!rec) chunk = B;
     // every chunk runs the layout the whole batch would
@@ -467,11 +472,12 @@ int solve_multi_t(ikg_model* model, int device, const void* targets, int64_t T_,
   if (a.collision && model->spec == ikg::kSpecNextage && !(params->lambda > 0) && !a.jit && rec_in_batch() &&
       rec_fits(nq) && params->variant != IKG_VARIANT_QUAD) {
     ikg::BatchArgs tmp{};
-    a.rec_chunk = rec_chunk<T>(*params, nq, T_, S);  // targets per launch (each with its S seeds)
+    a.rec_chunk = rec_chunk<T>(*params, T_, S);  // targets per launch (each with its S seeds)
     rec = offer_records<T>(model, tmp, *params, a.rec_chunk * S, nq, s, &rec_used);
     a.rec = tmp.rec;
     a.rec_n = tmp.rec_n;
     a.ck = tmp.ck;
+    a.rec_slots = tmp.rec_slots;
     a.rec_used = tmp.rec_used;
     if (!rec) a.rec_chunk = 0;
   }

@@ -1403,6 +1403,9 @@ struct TrajWs {
   T* ctab = nullptr;            // per problem, round -2's certificate for the resume kernel (ikg_solve.hpp kCtab)
   const uint64_t* rmask = nullptr;  // round 0: per problem and window, the iterates the resume kernel recorded
   int box = 1;                  // round -2: window boxes tested (IKG_BOX_COVER)
+  // round 0 after round -2: this launch scans list entries [rbase, rbase + rcap),
+  // whose records are in slots i - rbase (ikg_capi.hip records capacity)
+  int64_t rbase = 0, rcap = INT64_MAX;
 };
 
 // IKG_SCAN_CERT=0: the records scan without inscribed-ball certificates (A/B
@@ -1872,7 +1875,8 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
   const int nq = m->nq, RL = rec_len(m->n_passive);
   const int64_t par = (int64_t)(round & 1) * w.slots;
   rec_slots(m, lane, SL);
-  for (int i = blk; i < n; i += nb) {
+  const int i_end = (int)std::min<int64_t>(n, w.rbase + std::min<int64_t>(w.rcap, INT32_MAX));
+  for (int i = blk + (int)w.rbase; i < i_end; i += nb) {
     // answered by an earlier scan: window r - 1's, or (no pre-screen: witness0
     // null) the first checks' before window 0
     if ((round > 0 || (round == 0 && !witness0)) && w.done[i]) continue;  // wave-uniform
@@ -1922,7 +1926,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     const int nrec = nr & ~kTrajEnded;
     const bool ended = (nr & kTrajEnded) != 0;
     const int it0 = w.it0[ix];
-    T* rec = w.rec + ix * Wn * RL;
+    T* rec = w.rec + (w.wmask ? (int64_t)i - w.rbase : ix) * Wn * RL;  // round 0 after round -2: slot by list entry
 #ifdef IKG_CPROF
     // per-window counters, flushed once at the window's end (atomics inside the
     // loop would make the next load wait on them): 0 certificates, 1 positive,
@@ -2465,16 +2469,26 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
                          (const int32_t*)w.wit, tw, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out);
     }
     compact();
-    BatchArgs r = a;
-    r.rec_list = w.clist;
-    r.rec_count = w.count + 1;
-    r.rec_wmask = tw.wmask;
-    r.rec_ctab = tw.ctab;
-    r.rec_rmask = rmask;
-    ec = launch_pair_batch<T>(dm, prm, r, spec, s);
-    if (ec == hipSuccess) {
-      tw.wit_out = nullptr;
-      hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)scan_waves(a.B)), dim3(64), 0, s, dm, dc,
+    // the listed problems' records hold rec_slots problems (ikg_capi.hip
+    // records capacity): the resume kernel and the scan run in rounds of that
+    // many list entries -- launched for every round the batch could need, a
+    // round past the list's end exits at once
+    const int64_t cap = a.rec_slots > 0 ? std::min<int64_t>(a.rec_slots, a.B) : a.B;
+    tw.wit_out = nullptr;
+    for (int64_t rb = 0; rb < a.B && ec == hipSuccess; rb += cap) {
+      BatchArgs r = a;
+      r.rec_list = w.clist;
+      r.rec_count = w.count + 1;
+      r.rec_wmask = tw.wmask;
+      r.rec_ctab = tw.ctab;
+      r.rec_rmask = rmask;
+      r.rec_rbase = rb;
+      r.rec_rcap = cap;
+      ec = launch_pair_batch<T>(dm, prm, r, spec, s);
+      if (ec != hipSuccess) break;
+      tw.rbase = rb;
+      tw.rcap = cap;
+      hipLaunchKernelGGL((ikg_traj_scan_kernel<T>), dim3((unsigned)scan_waves(cap)), dim3(64), 0, s, dm, dc,
                          (const T*)a.targets, a.S, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
                          (const int32_t*)w.wit, tw, prm.max_iters + 1, 0, (T*)a.q_out, a.converged, a.iters,
                          (T*)a.err_out);

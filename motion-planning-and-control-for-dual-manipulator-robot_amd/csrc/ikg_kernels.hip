@@ -267,8 +267,13 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
       ra.wmask = a.rec_wmask;
       ra.ctab = (const T*)a.rec_ctab;
       ra.rmask = a.rec_rmask;
+      ra.rbase = a.rec_rbase;
+      ra.rcap = a.rec_rcap;
       // resume (a.rec_list): the same kernel over (listed problem, window) tasks, grid-stride
-      const dim3 g = a.rec_list ? dim3(resume_waves(a.B, rec_windows<T>(prm.max_iters), ppw)) : grid;
+      // resume: at most (windows x whole waves of the list) + one wave per first window, grid-stride
+      const int64_t nl = std::min<int64_t>(a.B, a.rec_rcap);
+      const int64_t rw = (int64_t)rec_windows<T>(prm.max_iters) * ((nl + ppw - 1) / ppw) + nl;
+      const dim3 g = a.rec_list ? dim3((unsigned)std::min<int64_t>(rw, 4096)) : grid;
       auto go = [&](auto kern) {
         hipLaunchKernelGGL(kern, g, dim3(64), lds_pad_bytes(), s, dmodel, prm, (const T*)a.targets,
                            (const T*)a.q0, a.q0_stride, a.B, a.S, ppw, (T*)a.q_out, a.converged, a.iters,
@@ -419,6 +424,7 @@ hipError_t launch_multistart(const KModel<T>* dmodel, const KParams<T>& prm, con
   b.rec = a.rec;
   b.rec_n = a.rec_n;
   b.ck = a.ck;
+  b.rec_slots = a.rec_slots;
   b.rec_used = a.rec_used;
   // AUTO keeps the pair layout here: seeds spread the update counts, and a
   // wave lasts as long as its slowest problem -- 64 per packed wave against 32

@@ -283,6 +283,8 @@ struct BatchArgs {
   const uint32_t* rec_wmask = nullptr;
   const void* rec_ctab = nullptr;   // per problem, the first check's certificate (ikg_solve.hpp kCtab)
   uint64_t* rec_rmask = nullptr;    // per problem and window, the iterates the resume kernel recorded
+  int64_t rec_rbase = 0, rec_rcap = 0;  // list entries [rbase, rbase + rcap) this resume launch regenerates
+  int64_t rec_slots = 0;        // records capacity: problems whose records `rec` holds (0: every problem of the launch)
   WsOwner* ws_owner = nullptr;  // scratch of captured solves (ws_alloc)
 };
 
@@ -320,6 +322,7 @@ struct MultiArgs {
   int32_t* rec_n = nullptr;
   void* ck = nullptr;
   bool* rec_used = nullptr;
+  int64_t rec_slots = 0;  // BatchArgs::rec_slots
   int64_t rec_chunk = 0;  // targets per launch when the records of all T x S problems exceed the budget (0: all)
 };
 

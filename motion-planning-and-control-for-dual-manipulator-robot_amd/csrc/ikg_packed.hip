@@ -55,12 +55,14 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
   if constexpr (REC == 2) {
     constexpr int K = kWinOf<float>;
     const int nw = rec_windows<float>(prm.max_iters);
-    const int64_t ntask = (int64_t)(*ra.count) * nw;
+    // this launch's list entries: [ra.rbase, ra.rbase + n), records in slots 0 .. n - 1
+    const int64_t n = max((int64_t)0, min((int64_t)*ra.count - ra.rbase, ra.rcap));
+    const int64_t ntask = n * nw;
     const int rl = rec_len(m->n_passive);
     for (int64_t t = (int64_t)blockIdx.x * 64 + threadIdx.x; t < ntask; t += (int64_t)gridDim.x * 64) {
       const int64_t i = t / nw;
       const int w = (int)(t - i * nw);
-      const int64_t p = ra.list[i];
+      const int64_t p = ra.list[ra.rbase + i];
       const int k0 = iters_out[p];
       if (w < k0 / K || !win_flagged(ra.wmask + p * mask_words<float>(prm.max_iters), w)) continue;
       const int64_t tgt = S > 1 ? p / S : p;
@@ -71,7 +73,7 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
       v2f qc = v2f{ckw[kCkQ], ckw[kCkArm + kCkQ]}, qa[kArmDof];
 #pragma unroll
       for (int k = 0; k < kArmDof; ++k) qa[k] = v2f{ckw[kCkQ + 1 + k], ckw[kCkArm + kCkQ + 1 + k]};
-      RecOut<float> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
+      RecOut<float> ro{ra.rec + i * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
                        q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl, ckw};
       ro.ctab = ra.ctab + p * kCtab;
       ro.rmask = ra.rmask + p * nw + w;
@@ -187,8 +189,10 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
   ra.wmask = a.rec_wmask;
   ra.ctab = (const float*)a.rec_ctab;
   ra.rmask = a.rec_rmask;
+  ra.rbase = a.rec_rbase;
+  ra.rcap = a.rec_rcap;
   // resume (a.rec_list): the instantiation the batch launch took (need from a.B), grid-stride over tasks
-  const dim3 g = a.rec_list ? dim3(resume_waves(a.B, rec_windows<float>(prm.max_iters), 64)) : grid;
+  const dim3 g = a.rec_list ? dim3(resume_waves(std::min<int64_t>(a.B, a.rec_rcap), rec_windows<float>(prm.max_iters), 64)) : grid;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, g, dim3(64), packed_lds_pad(), s, dmodel, prm, (const float*)a.targets,
                        (const float*)a.q0, a.q0_stride, a.B, a.S, (float*)a.q_out, a.converged, a.iters,

@@ -156,6 +156,7 @@ struct RecArgs {
   const uint32_t* wmask = nullptr;  // resume: per problem, the windows to regenerate (mask_words each)
   const T* ctab = nullptr;          // resume: per problem, the first check's certificate (kCtab values)
   uint64_t* rmask = nullptr;        // resume: per problem and window, the iterates recorded (rec_windows each)
+  int64_t rbase = 0, rcap = 0;      // resume: list entries [rbase, rbase + rcap), records in slots i - rbase
 };
 
 // Record-in-batch outputs of one problem (the REC batch kernels): the loop goes
@@ -288,8 +289,8 @@ __device__ __forceinline__ bool resume_covered(const typename LaneT<T>::E* __res
 // the record budget: no shared state, so a problem's checkpoints and answer do
 // not depend on which other problems share the launch or in what order they
 // run).  REC = 2 (resume): the loop restarts at a checkpoint and records the
-// window's iterates, with a per-lane update count (a resume wave's tasks
-// restart at different iterates).  The two are separate instantiations of the
+// window's iterates (the pair layout's waves hold tasks that start at the same
+// iterate, so the count stays wave-uniform).  The two are separate instantiations of the
 // same source; the compiler contracts a few products into FMAs differently in
 // them, so a regenerated iterate agrees with the batch loop's to the last bits
 // of q (fp64 ~1e-16), not bit for bit.  One instantiation serving both was
@@ -363,8 +364,8 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
 #if IKG_UNIFORM
     // every live lane of the wave has run the same number of updates, so the
     // count (and the resync / max_iters tests on it) is wave-uniform: scalar
-    // (not the resume kernels: their lanes restart at different iterates)
-    if constexpr (!is_packed<T> && REC != 2) it = __builtin_amdgcn_readfirstlane(it);
+    // (the pair layout's resume kernel too: a wave's tasks share their window)
+    if constexpr (!is_packed<T>) it = __builtin_amdgcn_readfirstlane(it);
 #endif
     // fp32: atan2f is as cheap as the tracked angle (measured)
     ThetaTrack<T>* tkp = (IKG_THETA_TRACK && is_f64<T>) ? &tk : nullptr;
@@ -600,19 +601,34 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
   const int lane = threadIdx.x;
   const int arm = lane & 1;
   if constexpr (REC == 2) {
+    // the update count stays wave-uniform (as in the batch loop): waves of
+    // range A hold one absolute window's tasks -- every listed problem's
+    // window w after its first passing iterate, all starting at w K -- ppw
+    // problems per wave (the list padded to whole waves per window); range B
+    // runs each problem's first window (from k0) in a wave of its own
     constexpr int K = kWinOf<T>;
     const int nw = rec_windows<T>(prm.max_iters);
-    const int64_t ntask = (int64_t)(*ra.count) * nw;
+    // this launch's list entries: [ra.rbase, ra.rbase + n), records in slots 0 .. n - 1
+    const int64_t n = max((int64_t)0, min((int64_t)*ra.count - ra.rbase, ra.rcap)), npad = (n + ppw - 1) / ppw * ppw;
+    const int64_t wavesA = (int64_t)nw * (npad / ppw), waves = wavesA + n;
     const int rl = rec_len(m->n_passive);
     const int64_t ckpp = ck_per_problem<T>(prm.max_iters);
-    for (int64_t t0 = (int64_t)blockIdx.x * ppw; t0 < ntask; t0 += (int64_t)gridDim.x * ppw) {
-      const int64_t t = t0 + (lane >> 1);
-      if (lane >= 2 * ppw || t >= ntask) continue;  // both lanes of a pair together
-      const int64_t i = t / nw;
-      const int w = (int)(t - i * nw);
-      const int64_t p = ra.list[i];
+    for (int64_t wv = blockIdx.x; wv < waves; wv += gridDim.x) {
+      int64_t i;
+      int w = -1;
+      if (wv < wavesA) {
+        w = (int)(wv / (npad / ppw));
+        i = (wv - (int64_t)w * (npad / ppw)) * ppw + (lane >> 1);
+        if (lane >= 2 * ppw || i >= n) continue;  // both lanes of a pair together
+      } else {
+        i = wv - wavesA;
+        if (lane >= 2) continue;
+      }
+      const int64_t p = ra.list[ra.rbase + i];
       const int k0 = iters_out[p];
-      if (w < k0 / K || !win_flagged(ra.wmask + p * mask_words<T>(prm.max_iters), w)) continue;
+      if (w < 0) w = k0 / K;  // range B: the first window
+      else if (w <= k0 / K) continue;
+      if (!win_flagged(ra.wmask + p * mask_words<T>(prm.max_iters), w)) continue;
       const int64_t tgt = S > 1 ? p / S : p;
       const int64_t row = S > 1 ? p - tgt * S : p;
       T RT[9], tT[3];
@@ -622,7 +638,7 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
       T qc = cq[0], qa[kArmDof];
 #pragma unroll
       for (int k = 0; k < kArmDof; ++k) qa[k] = cq[1 + k];
-      RecOut<T> ro{ra.rec + p * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
+      RecOut<T> ro{ra.rec + i * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
                    q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl, ckw};
       ro.ctab = ra.ctab + p * kCtab;
       ro.rmask = ra.rmask + p * nw + w;

@@ -396,14 +396,16 @@ def _close(a, b, tol):
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
 def test_record_chunks_give_the_one_launch_answer(csolver, dtype, monkeypatch):
-    """VERDICT r5 item 1 / ADVICE r5: a collision solve whose records exceed
-    the budget runs in chunks whose fixed slots fit it (ikg_capi.hip
-    rec_chunk), never from a shared pool, so a problem's answer does not depend
-    on the chunking or on wave order.  C2's 4,096 targets: one launch (the
-    default budget), and a 4 MB budget (fp64: 23 problems per launch, fp32: 47)
-    solved twice -- bit for bit equal; the same with every colliding problem's
-    records regenerated (IKG_BOX_COVER=0) and with the split first check
-    (IKG_PRESCAN=0: pre-screen + the window boxes over its list)."""
+    """VERDICT r5 item 1 / ADVICE r5: a collision solve never draws on a shared
+    pool, so a problem's answer does not depend on the chunking or on wave
+    order.  C2's 4,096 targets: one launch with one records round (the default
+    budgets); launch chunks whose checkpoints fit a 4 MB budget
+    (IKG_CK_BUDGET_MB: fp64 ~230 problems per launch); records rounds of a
+    4 MB records budget (IKG_REC_BUDGET_MB: fp64 26 listed problems per
+    round) -- each solved twice, all bit for bit equal.  The same with every
+    colliding problem's records regenerated (IKG_BOX_COVER=0) and with the
+    split first check (IKG_PRESCAN=0: pre-screen + the window boxes over its
+    list)."""
     from ikgrasp.workload import uniform_targets
     tg = uniform_targets(4096, seed=0)
     kw = dict(dtype=dtype, check_collision=True)
@@ -411,12 +413,13 @@ def test_record_chunks_give_the_one_launch_answer(csolver, dtype, monkeypatch):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         one = csolver.solve(tg, np.zeros(15), **kw)
-        monkeypatch.setenv("IKG_REC_BUDGET_MB", "4")
-        c1 = csolver.solve(tg, np.zeros(15), **kw)
-        c2 = csolver.solve(tg, np.zeros(15), **kw)
-        assert _same_bits(c1, c2), env
-        assert _same_bits(one, c1), env
-        monkeypatch.delenv("IKG_REC_BUDGET_MB")
+        for budget in ("IKG_CK_BUDGET_MB", "IKG_REC_BUDGET_MB"):
+            monkeypatch.setenv(budget, "4")
+            c1 = csolver.solve(tg, np.zeros(15), **kw)
+            c2 = csolver.solve(tg, np.zeros(15), **kw)
+            assert _same_bits(c1, c2), (env, budget)
+            assert _same_bits(one, c1), (env, budget)
+            monkeypatch.delenv(budget)
         for k in env:
             monkeypatch.delenv(k)
     assert 0 < int(one.converged.sum()) < 4096
@@ -464,29 +467,39 @@ def test_window_boxes_agree_with_full_regeneration(csolver, solve_cases, monkeyp
 
 
 def test_record_chunks_c3_fp32(csolver, monkeypatch):
-    """C3 (65,536 fp32, packed layout) with the collision term: its 5.2 GB of
-    records fit the default budget in one launch; under a 1 GiB budget the
-    batch runs as 6 chunks of ~10,923 problems, every chunk in the layout the
-    whole batch resolves to (packed), and gives the one launch's bits."""
+    """C3 (65,536 fp32, packed layout) with the collision term: its checkpoints
+    (570 MB) fit the default checkpoint budget in one launch and its listed
+    problems' records take several rounds of the 1 GiB records budget; under a
+    128 MB checkpoint budget the batch runs as 5 launch chunks, every chunk in
+    the layout the whole batch resolves to (packed), and a 64 MB records budget
+    takes ~80 rounds -- both give the one launch's bits."""
     from ikgrasp.workload import uniform_targets
     tg = uniform_targets(65536, seed=0)
     f = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
-    monkeypatch.setenv("IKG_REC_BUDGET_MB", "1024")
+    monkeypatch.setenv("IKG_CK_BUDGET_MB", "128")
     a = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
     assert _same_bits(f, a)
+    monkeypatch.delenv("IKG_CK_BUDGET_MB")
+    monkeypatch.setenv("IKG_REC_BUDGET_MB", "64")
+    b = csolver.solve(tg, np.zeros(15), dtype="f32", check_collision=True)
+    assert _same_bits(f, b)
 
 
 def test_multistart_record_chunks(csolver, solve_cases, monkeypatch):
     """A multi-start with the collision term splits over targets (each with its
-    S seeds) when the records exceed the budget: 64 targets x 4 seeds with a
-    2 MB budget (fp64: 3 targets per launch) equal the one-launch answer."""
+    S seeds) when the checkpoints exceed their budget, and runs its records in
+    rounds under a small records budget: 64 targets x 4 seeds with a 1 MB
+    checkpoint budget (fp64: 15 targets per launch), then a 2 MB records
+    budget, equal the one-launch answer."""
     c = solve_cases
     tg = c["targets"][:64]
     seeds = np.stack([np.zeros(15)] + [c["q0"][-k] for k in range(1, 4)])
     one = csolver.solve_multistart(tg, seeds, check_collision=True)
-    monkeypatch.setenv("IKG_REC_BUDGET_MB", "2")
-    ch = csolver.solve_multistart(tg, seeds, check_collision=True)
-    assert _same_bits(one, ch) and np.array_equal(one.best_seed, ch.best_seed)
+    for budget, mb in (("IKG_CK_BUDGET_MB", "1"), ("IKG_REC_BUDGET_MB", "2")):
+        monkeypatch.setenv(budget, mb)
+        ch = csolver.solve_multistart(tg, seeds, check_collision=True)
+        assert _same_bits(one, ch) and np.array_equal(one.best_seed, ch.best_seed), budget
+        monkeypatch.delenv(budget)
 
 
 @pytest.mark.parametrize("dtype", ["f64", "f32"])
