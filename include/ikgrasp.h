@@ -31,17 +31,27 @@
  *     throws or exits across this boundary.
  *   - Calls are re-entrant per (model, stream).
  *   - Results are deterministic: no answer depends on the order in which a
- *     launch's waves run.  A problem's fp64 answer is the same bit for bit in
- *     any batch size and batch position, with one exception below.  With the
- *     collision term, a problem that converges into collision runs on in the
- *     batch kernel itself, which records every later iterate into the
- *     problem's own fixed slot; a batch whose records exceed the record
- *     budget (IKG_REC_BUDGET_MB, 24 GiB) is solved as several launches of
- *     equal size whose records fit, every launch in the layout the whole
- *     batch would take, so the answer is the one-launch answer.  (Models the
- *     batch kernel does not record for -- generic or run-time-compiled
- *     kernels, lambda > 0, the QUAD layout -- run on in the trajectory
- *     kernel, which agrees with the records to rounding, q <= 1e-9.)  And in
+ *     launch's waves run, on the batch size or on a problem's position, with
+ *     the exceptions below.  With the collision term, a problem that
+ *     converges into collision runs on in the batch kernel itself, which
+ *     writes a checkpoint of its loop state per 32-update window into the
+ *     problem's own fixed slot; the scan proves windows colliding with a
+ *     certificate, and a window it cannot prove is regenerated from its
+ *     checkpoint by the same loop compiled as the resume kernel.  Which path
+ *     a problem takes is a function of that problem alone, so its answer is
+ *     the same in any batch, chunking (a batch whose checkpoints exceed their
+ *     budget, IKG_CK_BUDGET_MB, runs as equal launches in the whole batch's
+ *     layout) or records round (IKG_REC_BUDGET_MB); the regenerated iterates
+ *     agree with the batch loop's to rounding (the two instantiations
+ *     contract a few products into FMAs differently: flags and update counts
+ *     equal, q <= 1e-12 fp64 on the tests' batches).  Those kernels recompute
+ *     the carried joint trig exactly at every window start (every 32 updates
+ *     in fp64, 128 without the collision term), so a problem that never
+ *     collides gets the same answer as without the term to rounding, not bit
+ *     for bit.  (Models the batch
+ *     kernel does not record for -- generic or run-time-compiled kernels,
+ *     lambda > 0, the QUAD layout -- run on in the trajectory kernel, which
+ *     agrees with the batch loop to rounding, q <= 1e-9.)  And in
  *     fp64 a broadcast q0
  *     (q0_stride = 0) and per-problem q0 rows (and multi-start seeds)
  *     advance the joint sin/cos by different rules for steps of
@@ -73,9 +83,10 @@
  *     model owns (one per device it solves on).  The pool keeps up to
  *     1.25 GiB of freed memory reserved for the next solve (environment
  *     IKG_WS_KEEP_MB overrides the amount) and releases the rest at the next
- *     synchronisation.  The collision records are the large item: up to the
- *     record budget (24 GiB) while a collision solve runs, released after it
- *     beyond what the pool keeps.  ikg_model_trim synchronises each such device and
+ *     synchronisation.  A collision solve holds, while it runs, its window
+ *     checkpoints (17 KB per fp64 problem, 8.7 KB fp32, at max_iters 1,000)
+ *     and the records of the problems its scan regenerates, up to the
+ *     records budget (1 GiB).  ikg_model_trim synchronises each such device and
  *     releases everything the pools hold unused; ikg_model_destroy
  *     synchronises and destroys the pools.  Released memory goes back to the
  *     HIP runtime, which keeps it mapped for later pools and allocations of
