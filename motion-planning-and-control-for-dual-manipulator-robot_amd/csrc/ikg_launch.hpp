@@ -42,12 +42,19 @@ struct WsBuf {
   int dev;
   void* p;
   size_t bytes;
+  // recorded by the captured work at the buffer's last use (a node of the
+  // graph): a later capture reuses the buffer only once it has completed, so
+  // a launch of the destroyed graph still in flight keeps its scratch (ADVICE
+  // r5: a user object may be released before its exec's last launch ends).
+  hipEvent_t done = nullptr;
+  bool reuse = true;  // false: the record could not be captured -- never reused
 };
 
 struct WsState {
   static constexpr int kDevs = 64;
   std::mutex mu;
   std::vector<WsBuf> pending;     // buffers whose graphs are gone
+  std::vector<WsBuf> held;        // buffers of graphs still alive (their completion events)
   int64_t live = 0;               // buffers held by graphs
   hipMemPool_t pool[kDevs] = {};  // the model's scratch pools (ws_pool), per device
 };
@@ -65,7 +72,15 @@ inline void graph_scratch_release(void* arg) {  // user-object destructor: no HI
   GraphScratch* g = static_cast<GraphScratch*>(arg);
   {
     std::lock_guard<std::mutex> lock(g->st->mu);
-    g->st->pending.push_back(g->b);
+    WsBuf b = g->b;
+    for (size_t i = 0; i < g->st->held.size(); ++i)
+      if (g->st->held[i].p == b.p) {
+        b.done = g->st->held[i].done;
+        b.reuse = g->st->held[i].reuse;
+        g->st->held.erase(g->st->held.begin() + i);
+        break;
+      }
+    g->st->pending.push_back(b);
     --g->st->live;
   }
   delete g;
@@ -90,24 +105,34 @@ inline void ws_drain(WsOwner* owner) {
   (void)hipGetDevice(&prev);
   for (auto& b : v) {
     (void)hipSetDevice(b.dev);
-    (void)hipFree(b.p);
+    (void)hipFree(b.p);  // synchronises: every launch that used it has ended
+    if (b.done) (void)hipEventDestroy(b.done);
   }
   if (prev >= 0) (void)hipSetDevice(prev);
 }
 
-// The smallest pending buffer on `dev` of at least `bytes`, taken off the
-// list (a capture reuses it: no HIP call), or null.
-inline void* ws_take_pending(WsState& st, int dev, size_t bytes, size_t* got) {
+// The smallest pending buffer on `dev` of at least `bytes` whose last use has
+// completed (its event, queried outside capture semantics), taken off the
+// list for a capture to reuse, or null.
+inline void* ws_take_pending(WsState& st, int dev, size_t bytes, size_t* got, hipEvent_t* done) {
   std::lock_guard<std::mutex> lock(st.mu);
   int best = -1;
   for (int i = 0; i < (int)st.pending.size(); ++i) {
     const WsBuf& b = st.pending[i];
-    if (b.dev == dev && b.bytes >= bytes && (best < 0 || b.bytes < st.pending[best].bytes)) best = i;
+    if (b.dev != dev || b.bytes < bytes || (best >= 0 && b.bytes >= st.pending[best].bytes) || !b.done || !b.reuse)
+      continue;
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    const hipError_t q = hipEventQuery(b.done);
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    if (q == hipSuccess) best = i;
+    else if (q != hipErrorNotReady) (void)hipGetLastError();
   }
   if (best < 0) return nullptr;
   const WsBuf b = st.pending[best];
   st.pending.erase(st.pending.begin() + best);
   *got = b.bytes;
+  *done = b.done;
   return b.p;
 }
 
@@ -216,16 +241,25 @@ inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s
   (void)hipGetDevice(&dev);
   const size_t want = bytes ? bytes : 1;
   size_t got = want;
-  *p = ws_take_pending(*owner->st, dev, want, &got);  // a destroyed graph's buffer
+  hipEvent_t done = nullptr;
+  *p = ws_take_pending(*owner->st, dev, want, &got, &done);  // a destroyed graph's buffer, its last launch ended
   if (!*p) {
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     (void)hipThreadExchangeStreamCaptureMode(&mode);
     e = hipMalloc(p, want);
+    if (e == hipSuccess && hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      done = nullptr;
+    }
     (void)hipThreadExchangeStreamCaptureMode(&mode);
     if (e != hipSuccess) {
       *p = nullptr;
       return e;
     }
+  }
+  {
+    std::lock_guard<std::mutex> lock(owner->st->mu);
+    owner->st->held.push_back(WsBuf{dev, *p, got, done});
   }
   GraphScratch* g = new GraphScratch{owner->st, WsBuf{dev, *p, got}};
   hipUserObject_t uo = nullptr;
@@ -242,16 +276,34 @@ inline hipError_t ws_alloc(WsOwner* owner, void** p, size_t bytes, hipStream_t s
   delete g;
   {  // back on the pending list: freed by the next uncaptured call
     std::lock_guard<std::mutex> lock(owner->st->mu);
-    owner->st->pending.push_back(WsBuf{dev, *p, got});
+    for (size_t i = 0; i < owner->st->held.size(); ++i)
+      if (owner->st->held[i].p == *p) {
+        owner->st->held.erase(owner->st->held.begin() + i);
+        break;
+      }
+    owner->st->pending.push_back(WsBuf{dev, *p, got, done});
   }
   *p = nullptr;
   return e;
 }
 
-// the matching free: a captured solve's buffer stays with its graph
+// the matching free: a captured solve's buffer stays with its graph, and the
+// capture records its completion event after the buffer's last use (a failed
+// record drops the event: that buffer is then never reused by a capture)
 inline hipError_t ws_free(WsOwner* owner, void* p, hipStream_t s) {
   if (!p) return hipSuccess;
-  if (owner && stream_capturing(s)) return hipSuccess;
+  if (owner && stream_capturing(s)) {
+    std::lock_guard<std::mutex> lock(owner->st->mu);
+    for (auto& b : owner->st->held)
+      if (b.p == p && b.done) {
+        if (hipEventRecord(b.done, s) != hipSuccess) {
+          (void)hipGetLastError();
+          b.reuse = false;
+        }
+        break;
+      }
+    return hipSuccess;
+  }
   return hipFreeAsync(p, s);
 }
 
