@@ -1400,7 +1400,11 @@ struct TrajWs {
   int32_t* wit_out = nullptr;
   const T* ck = nullptr;        // the batch kernel's window checkpoints
   uint32_t* wmask = nullptr;    // per problem, the windows left (mask_words each): written by round -2, read by round 0
-  T* ctab = nullptr;            // per problem, round -2's certificate for the resume kernel (ikg_solve.hpp kCtab)
+  // round -2 over the whole batch: a problem with windows left is appended to
+  // this list (its order is the atomic's: no answer depends on it -- a
+  // problem's records, resume tasks and scan are its own), else compacted after
+  int32_t* app_list = nullptr;
+  int32_t* app_count = nullptr;
   const uint64_t* rmask = nullptr;  // round 0: per problem and window, the iterates the resume kernel recorded
   int box = 1;                  // round -2: window boxes tested (IKG_BOX_COVER)
   // round 0 after round -2: this launch scans list entries [rbase, rbase + rcap),
@@ -1776,39 +1780,6 @@ __device__ inline void window_covers(const KModel<T>* __restrict__ m, const KCol
     __syncthreads();
     scan_ball_cert(m, c, W.pair, RQ, SL, S.par, tgt, BC, S.L);
     const bool ok = BC.r > T(0);  // wave-uniform (LDS)
-    if (nc == 0) {  // the first passing iterate's certificate, as the resume kernel tests each iterate against it
-      T* tab = w.ctab + p * kCtab;
-      if (lane < 14) {
-        const int a = lane / 7, k = lane % 7;
-        const int slot = a == 0 ? k : (k == 0 ? -1 : kRecPass + k);
-        T qv = T(0), lv = T(0), in = T(0);
-        for (int e = 0; e < BC.n; ++e)
-          if (BC.off[e] == slot) {
-            qv = BC.qc[e];
-            lv = BC.lev[e];
-            in = T(1);
-          }
-        tab[a * kCkArm + kCtQc + k] = qv;
-        tab[a * kCkArm + kCtLev + k] = lv;
-        tab[a * kCkArm + kCtIn + k] = in;
-      } else if (lane == 14) {
-        T p0[2] = {T(0), T(0)}, p1[2] = {T(0), T(0)};  // passive joints at it = 0 (raw) and after (clamped)
-        for (int e = 0; e < BC.n; ++e)
-          if (BC.off[e] >= kRecPassive) {
-            const int pi = BC.off[e] - kRecPassive;
-            const T dr = fabs(PVr[pi] - BC.qc[e]), dc = fabs(PVc[pi] - BC.qc[e]);
-            p0[0] += dr;
-            p1[0] += dr * BC.lev[e];
-            p0[1] += dc;
-            p1[1] += dc * BC.lev[e];
-          }
-        tab[kCtR] = ok ? BC.r : T(-1);
-        tab[kCtPass] = p0[0];
-        tab[kCtPass + 1] = p1[0];
-        tab[kCtPass + 2] = p0[1];
-        tab[kCtPass + 3] = p1[1];
-      }
-    }
     int nxt = -1;
 #pragma unroll
     for (int k = 0; k < kCoverChunks; ++k) {
@@ -1820,7 +1791,6 @@ __device__ inline void window_covers(const KModel<T>* __restrict__ m, const KCol
     if (nxt < 0) break;
     wt = nxt;
   }
-  if (!boxes && lane == 0) w.ctab[p * kCtab + kCtR] = T(-1);  // no certificate: the resume kernel records every passing iterate
   bool any = false;
   uint32_t* wm = w.wmask + p * mask_words<T>(max_iters);
   const int nmw = mask_words<T>(max_iters);
@@ -1844,7 +1814,10 @@ __device__ inline void window_covers(const KModel<T>* __restrict__ m, const KCol
       iters[p] = max_iters;
     }
   }
-  if (lane == 0) w.wit_out[p] = any ? W.pair : -1;
+  if (lane == 0) {
+    w.wit_out[p] = any ? W.pair : -1;
+    if (any && w.app_list) w.app_list[atomicAdd(w.app_count, 1)] = (int32_t)p;
+  }
   __syncthreads();
 }
 
@@ -2429,10 +2402,9 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     const size_t bi = ((sizeof(int32_t) * (size_t)a.B + 255) & ~(size_t)255);
     const size_t bm = ((sizeof(uint32_t) * (size_t)mask_words<T>(prm.max_iters) * (size_t)a.B + 255) & ~(size_t)255);
     const size_t bc = ((sizeof(TrajCert<T>) * (size_t)a.B + 255) & ~(size_t)255);
-    const size_t bt = ((sizeof(T) * kCtab * (size_t)a.B + 255) & ~(size_t)255);
     const size_t br = ((sizeof(uint64_t) * (size_t)rec_windows<T>(prm.max_iters) * (size_t)a.B + 255) & ~(size_t)255);
     char* dws = nullptr;
-    e = ws_alloc(a.ws_owner, (void**)&dws, bi + bm + bc + bt + br, s);
+    e = ws_alloc(a.ws_owner, (void**)&dws, bi + bm + bc + br, s);
     if (e != hipSuccess) return e;
     TrajWs<T> tw{};
     tw.rec = (T*)a.rec;
@@ -2441,34 +2413,36 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     tw.done = (int32_t*)dws;
     tw.wmask = (uint32_t*)(dws + bi);
     tw.cst = (TrajCert<T>*)(dws + bi + bm);
-    tw.ctab = (T*)(dws + bi + bm + bc);
-    uint64_t* rmask = (uint64_t*)(dws + bi + bm + bc + bt);
+    uint64_t* rmask = (uint64_t*)(dws + bi + bm + bc);
     tw.rmask = rmask;
     tw.slots = a.B;
     tw.by_p = 1;
     tw.cert = scan_cert();
     tw.ck = (const T*)a.ck;
     tw.box = box_cover();
-    ws_trace("alloc scan", dws, bi + bm + bc + bt + br, s);
+    ws_trace("alloc scan", dws, bi + bm + bc + br, s);
     poison_int(dws, bi + bm + bc, s);
-    poison_float(tw.ctab, bt, s);
     poison_int(rmask, br, s);
     // `done` is only written (read by later rounds, of which there are none here), so it needs no fill
     tw.wit_out = w.wit;
-    if (first_fused(a.B)) {
+    if (first_fused(a.B)) {  // the listed problems appended by the kernel itself (no compaction launches)
+      TrajWs<T> tf = tw;
+      tf.app_list = w.clist;
+      tf.app_count = w.count + 1;
+      (void)hipMemsetAsync(w.count + 1, 0, sizeof(int32_t), s);
       hipLaunchKernelGGL((ikg_first_check_kernel<T>), dim3((unsigned)std::min<int64_t>(a.B, int64_t(1) << 20)), dim3(64),
                          0, s, dm, dc, (const T*)a.targets, a.S, a.B, (const int32_t*)nullptr,
-                         (const int32_t*)nullptr, (const int32_t*)nullptr, tw, (T*)a.q_out, a.converged, a.iters,
+                         (const int32_t*)nullptr, (const int32_t*)nullptr, tf, (T*)a.q_out, a.converged, a.iters,
                          (T*)a.err_out);
-    } else {  // pre-screen, its colliding list, the window boxes over it (rewriting w.wit in place)
+    } else {  // pre-screen, its colliding list, the window boxes over it (rewriting w.wit in place), compaction
       hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
                          (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
       compact();
       hipLaunchKernelGGL((ikg_first_check_kernel<T>), dim3((unsigned)scan_waves(a.B)), dim3(64), 0, s, dm, dc,
                          (const T*)a.targets, a.S, a.B, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
                          (const int32_t*)w.wit, tw, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out);
+      compact();
     }
-    compact();
     // the listed problems' records hold rec_slots problems (ikg_capi.hip
     // records capacity): the resume kernel and the scan run in rounds of that
     // many list entries -- launched for every round the batch could need, a
@@ -2480,7 +2454,6 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
       r.rec_list = w.clist;
       r.rec_count = w.count + 1;
       r.rec_wmask = tw.wmask;
-      r.rec_ctab = tw.ctab;
       r.rec_rmask = rmask;
       r.rec_rbase = rb;
       r.rec_rcap = cap;

@@ -265,7 +265,6 @@ static void launch_pair_batch_t(const KModel<T>* dmodel, const KParams<T>& prm, 
       ra.list = a.rec_list;
       ra.count = a.rec_count;
       ra.wmask = a.rec_wmask;
-      ra.ctab = (const T*)a.rec_ctab;
       ra.rmask = a.rec_rmask;
       ra.rbase = a.rec_rbase;
       ra.rcap = a.rec_rcap;

@@ -333,7 +333,6 @@ struct BatchArgs {
   const int32_t* rec_list = nullptr;
   const int32_t* rec_count = nullptr;
   const uint32_t* rec_wmask = nullptr;
-  const void* rec_ctab = nullptr;   // per problem, the first check's certificate (ikg_solve.hpp kCtab)
   uint64_t* rec_rmask = nullptr;    // per problem and window, the iterates the resume kernel recorded
   int64_t rec_rbase = 0, rec_rcap = 0;  // list entries [rbase, rbase + rcap) this resume launch regenerates
   int64_t rec_slots = 0;        // records capacity: problems whose records `rec` holds (0: every problem of the launch)

@@ -75,7 +75,6 @@ void ikg_packed_batch_kernel(const KModel<float>* __restrict__ m,
       for (int k = 0; k < kArmDof; ++k) qa[k] = v2f{ckw[kCkQ + 1 + k], ckw[kCkArm + kCkQ + 1 + k]};
       RecOut<float> ro{ra.rec + i * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
                        q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl, ckw};
-      ro.ctab = ra.ctab + p * kCtab;
       ro.rmask = ra.rmask + p * nw + w;
       ro.k0 = k0;
       ro.it_start = max(k0, w * K);
@@ -187,7 +186,6 @@ hipError_t launch_packed_batch(const KModel<float>* dmodel, const KParams<float>
   ra.list = a.rec_list;
   ra.count = a.rec_count;
   ra.wmask = a.rec_wmask;
-  ra.ctab = (const float*)a.rec_ctab;
   ra.rmask = a.rec_rmask;
   ra.rbase = a.rec_rbase;
   ra.rcap = a.rec_rcap;

@@ -134,17 +134,6 @@ template <typename E>
 IKG_HD inline int mask_words(int max_iters) { return (rec_windows<E>(max_iters) + 31) / 32; }
 IKG_HD inline bool win_flagged(const uint32_t* wm, int w) { return (wm[w >> 5] >> (w & 31)) & 1u; }
 
-// The first check's certificate as the resume kernel reads it (written by
-// ikg_collision.hip window_covers for a listed problem): per arm at
-// arm * kCkArm (the pair layout's lane; the packed layout's half) its 7
-// joints -- root (arm 0 only) and the arm's -- with the certified value, the
-// lever arm and whether the joint is on a chain the certificate bounds; the
-// radius (<= 0: none); the passive joints' fixed contribution, for an iterate
-// at it = 0 (raw) and after (clamped).  Each iterate's motion bound is then
-// ball_covers' over both sides together (the sum of both geometries' terms:
-// sound, slightly weaker than per side).
-constexpr int kCtQc = 0, kCtLev = 8, kCtIn = 16, kCtR = 64, kCtPass = 65, kCtab = 72;
-
 // Kernel argument of the record-writing (REC) batch kernels.
 template <typename T>
 struct RecArgs {
@@ -154,7 +143,6 @@ struct RecArgs {
   const int32_t* list = nullptr;    // resume launch: the problems whose windows are regenerated (null: the batch solve)
   const int32_t* count = nullptr;   // resume: list length (device)
   const uint32_t* wmask = nullptr;  // resume: per problem, the windows to regenerate (mask_words each)
-  const T* ctab = nullptr;          // resume: per problem, the first check's certificate (kCtab values)
   uint64_t* rmask = nullptr;        // resume: per problem and window, the iterates recorded (rec_windows each)
   int64_t rbase = 0, rcap = 0;      // resume: list entries [rbase, rbase + rcap), records in slots i - rbase
 };
@@ -175,7 +163,6 @@ struct RecOut {
   int rl;               // rec_len
   T* ck;                // its checkpoint slots (resume: the window's)
   int it_start = 0, k0 = -1, it_stop = 0;  // resume: first iterate, the problem's k0, one past the last iterate
-  const T* ctab = nullptr;    // resume: its certificate table
   uint64_t* rmask = nullptr;  // resume: this window's recorded iterates (bit j - first)
 };
 
@@ -253,35 +240,6 @@ __device__ __forceinline__ void ck_put(typename LaneT<T>::E* c, int arm, int off
     else
       store_block4(c + arm * kCkArm + off, v);
   }
-}
-
-template <typename T>
-__device__ __forceinline__ bool resume_covered(const typename LaneT<T>::E* __restrict__ tab, int arm, T qc,
-                                               const T* qa, int it) {
-  using E = typename LaneT<T>::E;
-  const E r = tab[kCtR];
-  T s0 = T(0), s1 = T(0);
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const T v = k == 0 ? qc : qa[k - 1];
-    const T qcv = ck_get<T>(tab, arm, kCtQc + k), lev = ck_get<T>(tab, arm, kCtLev + k),
-            in = ck_get<T>(tab, arm, kCtIn + k);
-    const T dd = fabs(v - qcv) * in;
-    s0 = s0 + dd;
-    s1 = s1 + dd * lev;
-  }
-  E a0, a1;
-  if constexpr (is_packed<T>) {
-    a0 = s0.x + s0.y;
-    a1 = s1.x + s1.y;
-  } else {
-    a0 = s0 + pair_swap(s0);
-    a1 = s1 + pair_swap(s1);
-  }
-  const int pc = it > 0 ? 2 : 0;
-  a0 += tab[kCtPass + pc];
-  a1 += tab[kCtPass + pc + 1];
-  return r > E(0) && a1 + r * a0 < r;
 }
 
 // REC = 1: from the first passing iterate on, the window checkpoints go into
@@ -437,8 +395,8 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
       if (k0 >= 0) {
         constexpr int K = kWinOf<E>;
         const int j = it - k0;
-        if constexpr (REC == 2) {  // a regenerated window: the passing iterates the certificate does not prove
-          if (pass && !resume_covered<T>(ro->ctab, arm, qc, qa, it)) {
+        if constexpr (REC == 2) {  // a regenerated window: its passing iterates (the scan tests only those)
+          if (pass) {
             put_record(recp + (int64_t)j * ro->rl);
             rbits |= 1ull << (it & (K - 1));
           }
@@ -640,7 +598,6 @@ __device__ inline void pair_batch_body(const KModel<T>* __restrict__ m, const KP
       for (int k = 0; k < kArmDof; ++k) qa[k] = cq[1 + k];
       RecOut<T> ro{ra.rec + i * (int64_t)(prm.max_iters + 1) * rl, ra.nrec + p, q0 + row * q0_stride,
                    q_out + p * m->nq, conv_out + p, iters_out + p, err_out + p * 2, rl, ckw};
-      ro.ctab = ra.ctab + p * kCtab;
       ro.rmask = ra.rmask + p * nw + w;
       ro.k0 = k0;
       ro.it_start = max(k0, w * K);
