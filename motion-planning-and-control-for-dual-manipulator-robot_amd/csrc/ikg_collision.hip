@@ -1410,7 +1410,18 @@ struct TrajWs {
   // round 0 after round -2: this launch scans list entries [rbase, rbase + rcap),
   // whose records are in slots i - rbase (ikg_capi.hip records capacity)
   int64_t rbase = 0, rcap = INT64_MAX;
+  // round 0 after round -2, split scan: a listed problem's 64-record chunks
+  // dealt round-robin to G waves (G from the listed count: about split_waves
+  // waves in all, at most kScanSplitMax per problem); each wave's first
+  // collision-free passing record goes to best[p] (atomicMin), and the last of
+  // the G waves to arrive (arrive[p]) writes the answer.  best / arrive are set
+  // by round -2 (fused) or by the host (split first check).  split_waves 0: off
+  int32_t* best = nullptr;
+  int32_t* arrive = nullptr;
+  int split_waves = 0;
 };
+constexpr int kScanSplitMax = 8;
+constexpr int32_t kScanNone = 0x7f7f7f7f;  // best[p] before any wave found an answer (a byte-fill value)
 
 // IKG_SCAN_CERT=0: the records scan without inscribed-ball certificates (A/B
 // knob, read at every launch so one process can compare both: the answers do
@@ -1442,6 +1453,12 @@ static bool first_fused(int64_t B) {
 static int box_cover() {
   const char* e = getenv("IKG_BOX_COVER");
   return e ? atoi(e) != 0 : 1;
+}
+// IKG_SCAN_SPLIT (read at every launch): the split scan's wave target (0: one
+// wave per listed problem)
+static int scan_split() {
+  const char* e = getenv("IKG_SCAN_SPLIT");
+  return e ? std::max(0, atoi(e)) : 2048;
 }
 static int64_t scan_waves(int64_t B) {
   const char* e = getenv("IKG_SCAN_WAVES");
@@ -1849,7 +1866,14 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
   const int64_t par = (int64_t)(round & 1) * w.slots;
   rec_slots(m, lane, SL);
   const int i_end = (int)std::min<int64_t>(n, w.rbase + std::min<int64_t>(w.rcap, INT32_MAX));
-  for (int i = blk + (int)w.rbase; i < i_end; i += nb) {
+  __shared__ int32_t sp_best;  // split scan: the answer of the last wave to arrive (-1: none), else -2
+  // split scan (round 0 after round -2): G waves per listed problem, the same G in every wave
+  const int n_ent = std::max(0, i_end - (int)w.rbase);
+  const int G = (!FIRST && round == 0 && w.wmask && w.by_p && w.best && w.split_waves > 0 && n_ent > 0)
+                    ? std::max(1, std::min(kScanSplitMax, w.split_waves / n_ent))
+                    : 1;
+  for (int64_t t = blk; t < (int64_t)n_ent * G; t += nb) {
+    const int i = (int)w.rbase + (int)(t / G), g = (int)(t % G);
     // answered by an earlier scan: window r - 1's, or (no pre-screen: witness0
     // null) the first checks' before window 0
     if ((round > 0 || (round == 0 && !witness0)) && w.done[i]) continue;  // wave-uniform
@@ -1858,6 +1882,10 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     // boxes), or with witness0 the pre-screen's colliding list (boxes only)
     const bool fused = FIRST && !witness0;
     const int64_t p = fused ? (int64_t)i : (int64_t)clist[i];
+    if (fused && w.best && lane == 0) {  // the split scan's per-problem state
+      w.best[p] = kScanNone;
+      w.arrive[p] = 0;
+    }
     if (fused && !conv[p]) {  // wave-uniform
       if (lane == 0) w.wit_out[p] = -1;
       continue;
@@ -1931,7 +1959,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
         S.cs[lane] = clampq(v, m->lo[pj], m->hi[pj]);  // every later one
       }
       __syncthreads();
-      for (int j = rstart + lane; j < nrec; j += 64)
+      for (int j = rstart + 64 * g + lane; j < nrec; j += 64 * G)  // this wave's chunks
         if (!wm || (win_flagged(wm, (it0 + j) / K) && ((rmw[(it0 + j) / K] >> ((it0 + j) & (K - 1))) & 1ull)))
           for (int k = 0; k < npv; ++k) rec[(int64_t)j * RL + kRecPassive + k] = it0 + j > 0 ? S.cs[k] : S.sn[k];
       __syncthreads();
@@ -1947,7 +1975,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
 #ifdef IKG_CPROF
     pc[11] += clock64() - cp0;  // passive columns
 #endif
-    for (int start = rstart; start < nrec && ans < 0; start += 64) {
+    for (int start = rstart + 64 * g; start < nrec && ans < 0; start += 64 * G) {
 #ifdef IKG_CPROF
       const unsigned long long cc0 = clock64();
 #endif
@@ -1955,6 +1983,12 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       // a record the resume kernel wrote: a window it regenerated, an iterate the certificate left
       const bool live = j < nrec && (!wm || (win_flagged(wm, (it0 + j) / K) &&
                                              ((rmw[(it0 + j) / K] >> ((it0 + j) & (K - 1))) & 1ull)));
+      if (G > 1) {  // another wave already answered before this chunk: nothing here can be the first
+        if (!__any(live)) continue;
+        const int b = __builtin_amdgcn_readfirstlane(__hip_atomic_load(w.best + p, __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT));
+        if (b < start) break;
+      }
       const T* r = rec + (int64_t)(live ? j : rstart) * RL;
       bool need = live && r[kRecPass] != T(0);
       // inscribed-ball certificates of the witness pair: every lane's motion
@@ -2054,20 +2088,47 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
       for (int k = 0; k < 12; ++k) atomicAdd(&g_scan[map[k]], pc[k]);
     }
 #endif
+    if (G > 1) {  // the last of the problem's G waves writes its answer: the first over all of them
+      if (lane == 0) {
+        if (ans >= 0) atomicMin(w.best + p, ans);
+        __threadfence();
+        const bool last = atomicAdd(w.arrive + p, 1) == G - 1;
+        __threadfence();
+        const int b = last ? atomicMin(w.best + p, kScanNone) : kScanNone;
+        sp_best = !last ? -2 : b < nrec ? b : -1;
+      }
+      __syncthreads();
+      ans = sp_best;
+      __syncthreads();
+      if (ans == -2) continue;  // wave-uniform: another of the problem's waves answers
+    }
     const int a = ans >= 0 ? ans : (ended ? nrec - 1 : -1);
     if (a >= 0) {  // final: the answer, or the iterate after max_iters (success = False)
       // the latter from the batch kernel's final record when its window was not regenerated
       const bool fin = ans < 0 && wm;
       const T* r = fin ? w.ck + p * ck_per_problem<T>(it0 + nrec - 1) + ck_final<T>(it0 + nrec - 1)
                        : rec + (int64_t)a * RL;
-      if (lane < nq) q_out[p * nq + lane] = (fin && SL[lane] >= kRecPassive) ? S.cs[SL[lane] - kRecPassive] : r[SL[lane]];
+      // a passive joint keeps its value in q_out (the batch kernels never move
+      // it), clamped from the first update on: not from S.sn / S.cs, which a
+      // full check (stage_trig_par) overwrites, nor from the record, whose
+      // passive slots another wave of a split scan fills
+      if (lane < nq) {
+        T v;
+        if (w.by_p && SL[lane] >= kRecPassive) {
+          v = q_out[p * nq + lane];
+          if (fin || it0 + a > 0) v = clampq(v, m->lo[lane], m->hi[lane]);
+        } else {
+          v = r[SL[lane]];
+        }
+        q_out[p * nq + lane] = v;
+      }
       if (lane < 2) err[p * 2 + lane] = sqrt(r[lane ? kRecErr1 : kRecErr0]);
       if (lane == 0) {
         conv[p] = ans >= 0 ? 1 : 0;
         iters[p] = it0 + a;
         w.done[i] = 1;
       }
-    } else if (lane == 0) {  // the witness carries over to the next window
+    } else if (lane == 0 && G == 1) {  // the witness carries over to the next window
       w.cst[i].pair = W.pair;
     }
     __syncthreads();
@@ -2404,7 +2465,7 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     const size_t bc = ((sizeof(TrajCert<T>) * (size_t)a.B + 255) & ~(size_t)255);
     const size_t br = ((sizeof(uint64_t) * (size_t)rec_windows<T>(prm.max_iters) * (size_t)a.B + 255) & ~(size_t)255);
     char* dws = nullptr;
-    e = ws_alloc(a.ws_owner, (void**)&dws, bi + bm + bc + br, s);
+    e = ws_alloc(a.ws_owner, (void**)&dws, bi + bm + bc + br + 2 * bi, s);
     if (e != hipSuccess) return e;
     TrajWs<T> tw{};
     tw.rec = (T*)a.rec;
@@ -2420,9 +2481,20 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     tw.cert = scan_cert();
     tw.ck = (const T*)a.ck;
     tw.box = box_cover();
-    ws_trace("alloc scan", dws, bi + bm + bc + br, s);
+    tw.split_waves = scan_split();
+    if (tw.split_waves > 0) {
+      tw.best = (int32_t*)(dws + bi + bm + bc + br);
+      tw.arrive = (int32_t*)(dws + bi + bm + bc + br + bi);
+    }
+    ws_trace("alloc scan", dws, bi + bm + bc + br + 2 * bi, s);
     poison_int(dws, bi + bm + bc, s);
     poison_int(rmask, br, s);
+    if (tw.best && !first_fused(a.B)) {  // the fused first check sets them per problem
+      (void)hipMemsetAsync(tw.best, 0x7f, sizeof(int32_t) * (size_t)a.B, s);
+      (void)hipMemsetAsync(tw.arrive, 0, sizeof(int32_t) * (size_t)a.B, s);
+    } else if (tw.best) {
+      poison_int(tw.best, 2 * bi, s);
+    }
     // `done` is only written (read by later rounds, of which there are none here), so it needs no fill
     tw.wit_out = w.wit;
     if (first_fused(a.B)) {  // the listed problems appended by the kernel itself (no compaction launches)

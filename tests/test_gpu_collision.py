@@ -466,6 +466,42 @@ def test_window_boxes_agree_with_full_regeneration(csolver, solve_cases, monkeyp
         assert 0 < int(a.converged.sum()) < 4096
 
 
+@pytest.mark.parametrize("case", ["f64", "f32", "packed", "multistart"])
+def test_split_scan_gives_the_one_wave_answer(csolver, solve_cases, monkeypatch, case):
+    """The records scan deals a listed problem's 64-record chunks to G waves
+    (IKG_SCAN_SPLIT: about that many waves in all, at most 8 per problem); the
+    answer is the first collision-free passing record over all of them, written
+    by the last wave to arrive.  It must be the one-wave scan's answer bit for
+    bit: IKG_SCAN_SPLIT=0 (one wave per problem), the default, and 65,536 (8
+    waves per problem), each solved twice with poisoned workspaces, also with
+    every colliding problem regenerated (IKG_BOX_COVER=0: the most records)."""
+    from ikgrasp import _lib
+    from ikgrasp.workload import uniform_targets
+    monkeypatch.setenv("IKG_POISON", "1")
+    tg = uniform_targets(4096, seed=0)
+    if case == "multistart":
+        c = solve_cases
+        seeds = np.stack([np.zeros(15)] + [c["q0"][-k] for k in range(1, 4)])
+        run = lambda: csolver.solve_multistart(tg[:1024], seeds, check_collision=True)
+    else:
+        kw = dict(dtype="f64" if case == "f64" else "f32", check_collision=True)
+        if case == "packed":
+            kw["variant"] = _lib.IKG_VARIANT_PACKED
+        run = lambda: csolver.solve(tg, np.zeros(15), **kw)
+    for box in ("1", "0"):
+        monkeypatch.setenv("IKG_BOX_COVER", box)
+        monkeypatch.setenv("IKG_SCAN_SPLIT", "0")
+        one = run()
+        for split in ("2048", "65536"):
+            monkeypatch.setenv("IKG_SCAN_SPLIT", split)
+            a = run()
+            assert _same_bits(a, run()), (box, split)
+            assert _same_bits(one, a), (box, split)
+            if case == "multistart":
+                assert np.array_equal(one.best_seed, a.best_seed)
+    assert 0 < int(one.converged.sum()) < one.converged.size
+
+
 def test_record_chunks_c3_fp32(csolver, monkeypatch):
     """C3 (65,536 fp32, packed layout) with the collision term: its checkpoints
     (570 MB) fit the default checkpoint budget in one launch and its listed
