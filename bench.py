@@ -337,9 +337,8 @@ def collision_kernels(kname, dtype, B, S=0):
     (ikg_capi.hip rec_chunk / offer_records, ikg_collision.hip
     launch_collide_continue): the batch kernel writing window checkpoints, in
     launches whose checkpoints fit their budget; then per launch the first
-    check with the window-box tests (ikg_traj_scan_kernel round -2: fused up to
-    65,536 problems, else the pre-screen and the boxes over its list), the
-    compaction, and per records round the resume launch of the batch kernel
+    check (the pre-screen, then the window-box tests over its list; fused with
+    IKG_PRESCAN=1), and per records round the resume launch of the batch kernel
     (windows left) and the records scan."""
     esz = 8 if dtype == "f64" else 4
     ck = esz * 64 * (1000 // 32 + 3) * max(S, 1)  # one unit's checkpoints (a target's S seeds)
@@ -350,12 +349,13 @@ def collision_kernels(kname, dtype, B, S=0):
     per = -(-B // chunks) * max(S, 1)  # problems per launch
     slots = max(1, (int(os.environ.get("IKG_REC_BUDGET_MB", str(REC_BUDGET_MB))) << 20) // rec)
     rounds = -(-per // min(per, slots))
-    fused = per <= 65536 if "IKG_PRESCAN" not in os.environ else os.environ["IKG_PRESCAN"] != "0"
+    fused = os.environ.get("IKG_PRESCAN", "0") != "0"
     label = (kname + " (window checkpoints past the first passing iterate) + " +
-             ("ikg_first_check_kernel (first check and window boxes)" if fused else
-              "ikg_prescreen_kernel + compaction + ikg_first_check_kernel (window boxes over its list)") +
-             " + ikg_compact_count_kernel + ikg_compact_write_kernel + " + kname +
-             f" (resume: windows left) + ikg_traj_scan_kernel (records scan), {rounds} records round(s)")
+             ("ikg_first_check_kernel (first check and window boxes, one wave per problem)" if fused else
+              "ikg_prescreen_kernel (first check, lists the colliding) + ikg_first_check_kernel (window boxes "
+              "over its list)") +
+             " + " + kname + f" (resume: windows left) + ikg_traj_scan_kernel (records scan, up to 8 waves per "
+             f"listed problem), {rounds} records round(s)")
     if chunks > 1:
         label += f"; {chunks} launch sequences of {per} problems (checkpoint budget {budget >> 20} MB)"
     return label, "the whole solve (all its kernels)"

@@ -1317,7 +1317,9 @@ __global__ __launch_bounds__(64) void ikg_prescreen_kernel(const KModel<T>* __re
                                                            const T* __restrict__ q, const T* __restrict__ targets,
                                                            int64_t S_per_target, int64_t B,
                                                            const uint8_t* __restrict__ conv,
-                                                           int32_t* __restrict__ witness) {
+                                                           int32_t* __restrict__ witness,
+                                                           int32_t* __restrict__ app_list = nullptr,
+                                                           int32_t* __restrict__ app_count = nullptr) {
   __shared__ CollideScratch<T> S;
   __shared__ T tgt[12];
   __shared__ Witness<T> W;
@@ -1349,7 +1351,10 @@ __global__ __launch_bounds__(64) void ikg_prescreen_kernel(const KModel<T>* __re
 #else
   const bool col = collide_wave<T, true>(m, c, S, tgt, W);
 #endif
-  if (lane == 0) witness[p] = col ? W.pair : -1;
+  if (lane == 0) {
+    witness[p] = col ? W.pair : -1;
+    if (col && app_list) app_list[atomicAdd(app_count, 1)] = (int32_t)p;  // colliding: listed (no compaction)
+  }
 }
 
 // ---------------------------------------------------------------- trajectory-first continuation
@@ -1440,15 +1445,19 @@ static int scan_cert() {
 // so every problem that collides at its first passing iterate has all its
 // records regenerated and scanned -- the round-5 records' work, for the tests
 // that pin the window form's answers to it (and for A/Bs)
-// The first check of a records solve (ikg_first_check_kernel): fused with the
-// window boxes over the whole batch up to 65,536 problems per launch; above,
-// the lean pre-screen kernel checks every converged problem and the boxes run
-// over its colliding list (the fused kernel's registers -- certificate code --
-// hold it to 1 wave per SIMD in fp64: 1.6 ms for C4's 131,072-problem share).
-// IKG_PRESCAN=1/0 (read at every launch) forces the fused / split form.
+// The first check of a records solve: the lean pre-screen kernel checks every
+// converged problem and lists the colliding ones itself, then
+// ikg_first_check_kernel runs the window boxes over that list.  The fused form
+// (IKG_PRESCAN=1, read at every launch: one wave per problem of the batch for
+// both) carries the certificate code's registers into every problem's check --
+// 1 wave per SIMD in fp64, 1.6 ms for C4's 131,072-problem share; with the
+// kernels' own appends (no compaction launches) the split form is also the
+// faster at C2 (70 against 75 us) and C3 (254 against 267 us),
+// profiles/r06/records/prescan/
 static bool first_fused(int64_t B) {
+  (void)B;
   const char* e = getenv("IKG_PRESCAN");
-  return e ? atoi(e) != 0 : B <= 65536;
+  return e ? atoi(e) != 0 : false;
 }
 static int box_cover() {
   const char* e = getenv("IKG_BOX_COVER");
@@ -1882,7 +1891,7 @@ __device__ __forceinline__ void traj_scan_body(const KModel<T>* __restrict__ m, 
     // boxes), or with witness0 the pre-screen's colliding list (boxes only)
     const bool fused = FIRST && !witness0;
     const int64_t p = fused ? (int64_t)i : (int64_t)clist[i];
-    if (fused && w.best && lane == 0) {  // the split scan's per-problem state
+    if (FIRST && w.best && lane == 0) {  // the split scan's per-problem state (a listed problem passes here)
       w.best[p] = kScanNone;
       w.arrive[p] = 0;
     }
@@ -2164,8 +2173,11 @@ void ikg_traj_update_kernel(const KModel<T>* __restrict__ m, KParams<T> prm,
 // check at the batch kernel's iterate and the window boxes (window_covers);
 // with witness0, over the pre-screen's colliding list (clist, *count): the
 // window boxes only
+#ifndef IKG_FC_WAVES64  // timing knob: waves per SIMD the fp64 first check and records scan are compiled for
+#define IKG_FC_WAVES64 1
+#endif
 template <typename T>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 3 : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 3 : IKG_FC_WAVES64)))
 void ikg_first_check_kernel(const KModel<T>* __restrict__ m, const KCollision<T>* __restrict__ c,
                             const T* __restrict__ targets, int64_t S_per_target, int64_t B,
                             const int32_t* __restrict__ clist, const int32_t* __restrict__ count,
@@ -2178,7 +2190,7 @@ void ikg_first_check_kernel(const KModel<T>* __restrict__ m, const KCollision<T>
 // fp32: at most 168 VGPRs, so 3 waves fit a SIMD as before the certificate
 // code (which alone would take the kernel to 182 and 2 waves)
 template <typename T>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 3 : 1)))
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 4 ? 3 : IKG_FC_WAVES64)))
 void ikg_traj_scan_kernel(const KModel<T>* __restrict__ m,
                                                            const KCollision<T>* __restrict__ c,
                                                            const T* __restrict__ targets, int64_t S_per_target,
@@ -2489,31 +2501,27 @@ hipError_t launch_collide_continue(const KModel<T>* dm, const KCollision<T>* dc,
     ws_trace("alloc scan", dws, bi + bm + bc + br + 2 * bi, s);
     poison_int(dws, bi + bm + bc, s);
     poison_int(rmask, br, s);
-    if (tw.best && !first_fused(a.B)) {  // the fused first check sets them per problem
-      (void)hipMemsetAsync(tw.best, 0x7f, sizeof(int32_t) * (size_t)a.B, s);
-      (void)hipMemsetAsync(tw.arrive, 0, sizeof(int32_t) * (size_t)a.B, s);
-    } else if (tw.best) {
-      poison_int(tw.best, 2 * bi, s);
-    }
+    if (tw.best) poison_int(tw.best, 2 * bi, s);  // the first check sets them for every problem it may list
     // `done` is only written (read by later rounds, of which there are none here), so it needs no fill
     tw.wit_out = w.wit;
-    if (first_fused(a.B)) {  // the listed problems appended by the kernel itself (no compaction launches)
-      TrajWs<T> tf = tw;
-      tf.app_list = w.clist;
-      tf.app_count = w.count + 1;
-      (void)hipMemsetAsync(w.count + 1, 0, sizeof(int32_t), s);
+    // the problems with windows left are appended to w.clist (count w.count[1])
+    // by the kernels themselves (no compaction launches; the order is the
+    // atomics', and no answer depends on it)
+    TrajWs<T> tf = tw;
+    tf.app_list = w.clist;
+    tf.app_count = w.count + 1;
+    (void)hipMemsetAsync(w.count + 1, 0, 2 * sizeof(int32_t), s);
+    if (first_fused(a.B)) {  // one wave per problem of the batch: the first check and the window boxes
       hipLaunchKernelGGL((ikg_first_check_kernel<T>), dim3((unsigned)std::min<int64_t>(a.B, int64_t(1) << 20)), dim3(64),
                          0, s, dm, dc, (const T*)a.targets, a.S, a.B, (const int32_t*)nullptr,
                          (const int32_t*)nullptr, (const int32_t*)nullptr, tf, (T*)a.q_out, a.converged, a.iters,
                          (T*)a.err_out);
-    } else {  // pre-screen, its colliding list, the window boxes over it (rewriting w.wit in place), compaction
+    } else {  // the pre-screen lists the colliding (w.list, count w.count[2]), the window boxes run over that list
       hipLaunchKernelGGL((ikg_prescreen_kernel<T>), dim3((unsigned)a.B), dim3(64), 0, s, dm, dc, (const T*)a.q_out,
-                         (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit);
-      compact();
+                         (const T*)a.targets, a.S, a.B, (const uint8_t*)a.converged, w.wit, w.list, w.count + 2);
       hipLaunchKernelGGL((ikg_first_check_kernel<T>), dim3((unsigned)scan_waves(a.B)), dim3(64), 0, s, dm, dc,
-                         (const T*)a.targets, a.S, a.B, (const int32_t*)w.clist, (const int32_t*)(w.count + 1),
-                         (const int32_t*)w.wit, tw, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out);
-      compact();
+                         (const T*)a.targets, a.S, a.B, (const int32_t*)w.list, (const int32_t*)(w.count + 2),
+                         (const int32_t*)w.wit, tf, (T*)a.q_out, a.converged, a.iters, (T*)a.err_out);
     }
     // the listed problems' records hold rec_slots problems (ikg_capi.hip
     // records capacity): the resume kernel and the scan run in rounds of that

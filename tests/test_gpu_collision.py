@@ -404,12 +404,13 @@ def test_record_chunks_give_the_one_launch_answer(csolver, dtype, monkeypatch):
     4 MB records budget (IKG_REC_BUDGET_MB: fp64 26 listed problems per
     round) -- each solved twice, all bit for bit equal.  The same with every
     colliding problem's records regenerated (IKG_BOX_COVER=0) and with the
-    split first check (IKG_PRESCAN=0: pre-screen + the window boxes over its
-    list)."""
+    fused first check (IKG_PRESCAN=1: one wave per problem of the batch for the
+    check and the window boxes; the default pre-screens and runs the boxes over
+    its list)."""
     from ikgrasp.workload import uniform_targets
     tg = uniform_targets(4096, seed=0)
     kw = dict(dtype=dtype, check_collision=True)
-    for env in ({}, {"IKG_BOX_COVER": "0"}, {"IKG_PRESCAN": "0"}):
+    for env in ({}, {"IKG_BOX_COVER": "0"}, {"IKG_PRESCAN": "1"}):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         one = csolver.solve(tg, np.zeros(15), **kw)
