@@ -78,6 +78,9 @@ __device__ __forceinline__ void load_block8(const T* src, T (&v)[8]) {
 
 template <typename T>
 __device__ __forceinline__ void store_block4(T* dst, const T (&v)[4]) {
+#if defined(IKG_REC_NOSTORE)  // timing ablation only
+  (void)dst, (void)v;
+#else
   struct alignas(16) V16 {
     T x[16 / sizeof(T)];
   };
@@ -89,6 +92,7 @@ __device__ __forceinline__ void store_block4(T* dst, const T (&v)[4]) {
     for (int e = 0; e < per; ++e) b.x[e] = v[k * per + e];
     reinterpret_cast<V16*>(dst)[k] = b;
   }
+#endif
 }
 
 // ---- window checkpoints (round 6: the records' window form)
@@ -121,7 +125,11 @@ constexpr int kCkQ = 0, kCkSn = 8, kCkCs = 16, kCkTk = 24, kCkL = 7;
 template <typename E>
 constexpr int kWinOf = kWin;
 template <typename T>
+#ifdef IKG_REC_RS_ABL  // timing ablation only: the batch loop's own resync period (resumed windows wrong)
+constexpr int kRsRec = Trig<T>::kResync;
+#else
 constexpr int kRsRec = Trig<T>::kResync < kWin ? Trig<T>::kResync : kWin;  // divides kWin
+#endif
 template <typename E>
 IKG_HD inline int rec_windows(int max_iters) { return max_iters / kWinOf<E> + 1; }
 template <typename E>
@@ -457,12 +465,14 @@ __device__ inline bool solve_pair(const KModel<typename LaneT<T>::E>* __restrict
     sc_acc[2] += sc_t1 - sc_t0;
 #endif
     arm_update(m, arm, T(prm.dt), s, dq, qc, qa, limp);
+#ifndef IKG_REC_NOL_ABL  // timing ablation only: no path length (window boxes wrong)
     if constexpr (REC == 1) {  // the window's path length: this update's largest joint step
       T mv = fabs(qc - q_old[0]);
 #pragma unroll
       for (int k = 0; k < kArmDof; ++k) mv = fmax(mv, fabs(qa[k] - q_old[k + 1]));
       L = L + mv;
     }
+#endif
     ++it;
 #ifdef IKG_STAGE_CLOCK
     IKG_STAMP(sc_t0);
