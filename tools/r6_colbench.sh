@@ -3,7 +3,7 @@
 # line, re-run after tools/pmc_summary.py regenerated profiles/pmc_*_col.json
 # (the lines read their `traffic` from those): gpurun -- bash tools/r6_colbench.sh
 set -o pipefail
-O=gpurun_out/r6col; mkdir -p $O
+O=gpurun_out/${TAG:-r6col}; mkdir -p $O
 b() { n=$1; shift; timeout -k 10 300 python bench.py --no-cpu-baseline --no-extra "$@" > $O/bench_$n.json 2>> $O/bench.err || exit 1; }
 b c2col --collision --steps 20
 b c3col_f32 --collision --dtype f32 --batch 65536
