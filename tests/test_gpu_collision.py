@@ -503,6 +503,37 @@ def test_split_scan_gives_the_one_wave_answer(csolver, solve_cases, monkeypatch,
     assert 0 < int(one.converged.sum()) < one.converged.size
 
 
+@pytest.mark.parametrize("case", ["f64", "f32", "packed"])
+def test_collision_answers_keep_clamped_passive_joints(csolver, monkeypatch, case):
+    """The passive head joints (tools.py:21-22: zero Jacobian columns) only
+    move by the first update's clamp, so every answer of a collision solve --
+    the first passing iterate, a later collision-free one, or the iterate
+    after max_iters -- holds the clamped seed values.  The scan writes them
+    from q_out (a full check's trig staging reuses the scratch the passive
+    values were staged in); seeds outside the head limits make a wrong source
+    visible.  Default scan, one wave per problem, and every colliding problem
+    regenerated (IKG_BOX_COVER=0: the most full checks)."""
+    from ikgrasp import _lib
+    from ikgrasp.workload import uniform_targets
+    from oracle import ik_oracle as o
+    tg = uniform_targets(4096, seed=0)
+    q0 = np.zeros(15)
+    q0[1], q0[2] = 5.0, -5.0  # outside HEAD_JOINT0/1 limits
+    kw = dict(dtype="f64" if case == "f64" else "f32", check_collision=True)
+    if case == "packed":
+        kw["variant"] = _lib.IKG_VARIANT_PACKED
+    for env in ({}, {"IKG_SCAN_SPLIT": "0"}, {"IKG_BOX_COVER": "0"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        sol = csolver.solve(tg, q0, **kw)
+        assert (sol.iters > 0).all()
+        assert (sol.q[:, 1] == np.float32(o.UPPER[1]) if case != "f64" else sol.q[:, 1] == o.UPPER[1]).all(), env
+        assert (sol.q[:, 2] == np.float32(o.LOWER[2]) if case != "f64" else sol.q[:, 2] == o.LOWER[2]).all(), env
+        assert 0 < int(sol.converged.sum()) < 4096
+        for k in env:
+            monkeypatch.delenv(k)
+
+
 def test_record_chunks_c3_fp32(csolver, monkeypatch):
     """C3 (65,536 fp32, packed layout) with the collision term: its checkpoints
     (570 MB) fit the default checkpoint budget in one launch and its listed
