@@ -104,8 +104,24 @@ struct Shape {
   int kind;
 };
 
+// IKG_SUPPORT_RELOAD (default 1): the placement's rotation and translation are
+// re-read from LDS at every support call.  Held in registers across the GJK
+// loop (the compiler hoists the loads: 2 x 12 values) they took the fp64 check
+// kernels -- pre-screen, window boxes, records scan -- past 256 registers
+// (248-256 VGPRs + 18 AGPRs: one wave per SIMD); re-read they fit 2 waves
+// (244-256 VGPRs, no AGPRs): C4 share + collision 6.97 -> 6.11 ms, C2 + collision
+// 1.259 -> 1.248 (profiles/r06/records/reload/).  fp32 (3 waves per SIMD either
+// way) keeps the hoisted loads: C3 unchanged, C5 within +-1%.  The values and
+// the arithmetic are the same: answers bit for bit.
+#ifndef IKG_SUPPORT_RELOAD
+#define IKG_SUPPORT_RELOAD 1
+#endif
 template <typename T>
-IKG_HD inline void shape_support(const Shape<T>& s, const T* d, T* out) {
+IKG_HD inline void shape_support(const Shape<T>& s0, const T* d, T* out) {
+  Shape<T> s = s0;
+#if defined(__HIP_DEVICE_COMPILE__) && IKG_SUPPORT_RELOAD
+  if constexpr (sizeof(T) == 8) asm volatile("" : "+v"(s.R), "+v"(s.t));  // opaque pointers: the loads stay in the loop
+#endif
   if (s.kind == kSphere) {
     const T n2 = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     const T f = n2 > T(0) ? s.dims[0] / sqrt(n2) : T(0);
